@@ -1,0 +1,123 @@
+/*
+ * include/pnrt.h -- C ABI of libpnrt.so, the MI355X (gfx950) path-tracing
+ * library that replaces PnRayTracing's OpenGL compute-shader hot path
+ * (shaders/ray_tracing.comp, dispatched from main.cpp:613).
+ *
+ * Each entry point replaces one piece of the GL binding contract main.cpp
+ * fills today (the reference interface is cited per function).  Inputs are the
+ * SAME host-built float arrays main.cpp uploads (integers stored as floats);
+ * the library copies caller memory during upload* and never keeps pointers to
+ * it.  No torch or HIP types appear in the signatures: streams are passed as
+ * opaque pointers (a hipStream_t, or NULL for the context's own stream).
+ *
+ * Threading: a context belongs to one HIP device and is not thread-safe; use
+ * one context per device (one process per GPU in the multi-GPU driver).
+ * Errors: every int-returning call returns 0 on success or a negative PNRT_E*
+ * code, with a message in pnrt_last_error(ctx).  Nothing calls exit().
+ */
+#ifndef PNRT_H
+#define PNRT_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNRT_OK 0
+#define PNRT_E_ARG (-1)       /* invalid argument                      */
+#define PNRT_E_HIP (-2)       /* HIP runtime error                     */
+#define PNRT_E_STATE (-3)     /* call out of order (e.g. render before upload) */
+#define PNRT_E_SCENE (-4)     /* scene arrays inconsistent / unsupported */
+#define PNRT_E_NOMEM (-5)
+
+typedef struct pnrt_ctx pnrt_ctx;
+
+/* camera.hpp:28-30 / the camera.* uniforms set at main.cpp:606-610 */
+typedef struct {
+    float eye[3], lower_left[3], horizontal[3], vertical[3];
+} pnrt_camera;
+
+typedef struct {
+    int n_interior;      /* interior BVH nodes in the device layout          */
+    int n_triangles;
+    int max_depth;       /* deepest reference node (root = 0)                */
+    int64_t device_bytes;/* scene bytes resident in HBM                      */
+    int root_is_leaf;
+    int stack_limit;     /* traversal stack entries available per lane       */
+} pnrt_device_info;
+
+/* Traversal options (pnrt_set_options). */
+#define PNRT_TRAVERSE_EXACT 0   /* the reference's box visits (no tMax culling)      */
+#define PNRT_TRAVERSE_ZCULL 1   /* + provably result-neutral z-slab culling (default) */
+
+const char* pnrt_version(void);
+
+/* Replaces WindowInit's GL context (main.cpp:64-94): bind HIP device. */
+int pnrt_create(int device, pnrt_ctx** out);
+void pnrt_destroy(pnrt_ctx* ctx);
+const char* pnrt_last_error(pnrt_ctx* ctx);
+/* Launch work on `hip_stream` (a hipStream_t; NULL = the context's stream). */
+int pnrt_set_stream(pnrt_ctx* ctx, void* hip_stream);
+
+/* Replaces the five TBO/texture uploads main.cpp:409-524 (texture units 0-4)
+ * and the lightsSize/lightsSumArea uniforms (main.cpp:391-392):
+ *   vertices  15 f each (main.cpp:412-428)     materials 18 f (main.cpp:438-456)
+ *   triangles  6 f each (main.cpp:470-477)     bvh_nodes 12 f (main.cpp:488-501)
+ *   lights     3 f each (main.cpp:513-517)     (lights may be NULL when n_lights = 0)
+ * The arrays are validated and re-laid out for gfx950. */
+int pnrt_upload_scene(pnrt_ctx* ctx,
+                      const float* vertices, int n_vertices,
+                      const float* materials, int n_materials,
+                      const float* triangles, int n_triangles,
+                      const float* bvh_nodes, int n_nodes,
+                      const float* lights, int n_lights, float lights_sum_area);
+
+/* Replaces the albedo texture uploads (main.cpp:527-554, units 5..24):
+ * tightly packed 8-bit rows as stbi_load returns them; GL's default
+ * UNPACK_ALIGNMENT of 4 is applied as glTexImage2D would. slot 0..19. */
+int pnrt_upload_texture(pnrt_ctx* ctx, int slot, const uint8_t* pixels, int width, int height,
+                        int channels);
+
+/* Replaces LoadHDRImage's two glTexImage2D calls (shader.hpp:136-214, units
+ * 29/30) and the HDRImageWidth/Height/HasHDRImage uniforms.  hdr_rgb == NULL
+ * clears the environment (HasHDRImage = 0). */
+int pnrt_upload_env(pnrt_ctx* ctx, const float* hdr_rgb, const float* random_hdr_rgb, int width,
+                    int height);
+
+/* Replaces the per-frame uniforms SCREEN_WIDTH/HEIGHT (main.cpp:389-390),
+ * camera.* (main.cpp:606-610) and MAX_BOUNCE_DEPTH (main.cpp:593,599).
+ * (Re)allocates a zeroed width*height RGBA32F accumulation image when the
+ * size changes. */
+int pnrt_set_frame(pnrt_ctx* ctx, int width, int height, const pnrt_camera* camera,
+                   int max_bounce_depth);
+
+int pnrt_set_options(pnrt_ctx* ctx, int traverse_mode);
+
+/* Replaces glDispatchCompute (main.cpp:613) called once per frame for frames
+ * first_frame .. first_frame + n_frames - 1 (frameCount uniform), blended in
+ * order into the accumulation image with the progressive mean of
+ * ray_tracing.comp:988-991.  Shard selector (multi-GPU row bands): only rows
+ * y with (y / band_rows) % n_shards == shard are rendered; full image =
+ * (band_rows >= 1, n_shards = 1, shard = 0).  Asynchronous on the stream. */
+int pnrt_render(pnrt_ctx* ctx, uint32_t first_frame, uint32_t n_frames, int band_rows,
+                int n_shards, int shard);
+
+/* Redraw semantics (main.cpp:592-596): zero the accumulation image. */
+int pnrt_reset_accum(pnrt_ctx* ctx);
+/* Synchronise and copy the width*height*4 floats (row 0 = bottom) to host. */
+int pnrt_read_accum(pnrt_ctx* ctx, float* rgba_out);
+/* Device pointer of the accumulation image (for collectives / zero-copy use). */
+void* pnrt_accum_device_ptr(pnrt_ctx* ctx);
+/* Copy this shard's rows, in increasing y, into a contiguous device buffer
+ * (rows_of_shard * width * 4 floats), on the context stream. */
+int pnrt_pack_rows(pnrt_ctx* ctx, void* dst_device, int band_rows, int n_shards, int shard);
+int pnrt_synchronize(pnrt_ctx* ctx);
+int pnrt_get_device_info(pnrt_ctx* ctx, pnrt_device_info* info);
+
+/* Test hook: evaluate one PN-libm / IEEE primitive on the device (same fn
+ * codes as the oracle's pno_math_eval); host in/out arrays of n floats. */
+int pnrt_debug_math(pnrt_ctx* ctx, int fn, const float* a, const float* b, float* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,78 @@
+"""In-tree build of the native libraries (no JIT cache, nothing installed).
+
+    libpnrt_host.so  g++   csrc/host/pnrt_host.cpp          (host scene library)
+    libpnrt.so       hipcc csrc/pnrt_device.hip, gfx950     (device library)
+    oracle/liboracle.so    gcc (TEST-ONLY parity oracle; see oracle/)
+    oracle/_ref/ref_driver g++ on /root/reference headers (only where present)
+
+Floating point: every library is built with -ffp-contract=off and without
+fast-math so the HIP kernel, the host library and the oracle evaluate the
+same IEEE binary32 operation sequences (bit-exact parity).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INC = os.path.join(REPO, "include")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PNRT_OFFLOAD_ARCH", "gfx950")
+
+DEVICE_SRCS = ["pnrt_device.hip"]
+DEVICE_DEPS = ["pnrt_device.hip", "pt_common.h", "pt_kernel.h", "pt_shade.h", "pn_math.h", "sobol_v.inc"]
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True, cwd=cwd)
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_host(force=False):
+    out = os.path.join(PKG, "libpnrt_host.so")
+    src = os.path.join(CSRC, "host", "pnrt_host.cpp")
+    if force or _stale(out, [src, os.path.join(INC, "pnrt_host.h")]):
+        _run(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+              "-Wall", "-I", INC, src, "-o", out])
+    return out
+
+
+def build_device(force=False, extra=()):
+    out = os.path.join(PKG, "libpnrt.so")
+    deps = [os.path.join(CSRC, d) for d in DEVICE_DEPS] + [os.path.join(INC, "pnrt.h")]
+    if force or extra or _stale(out, deps):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-rdc", "-I", INC,
+               *extra, *[os.path.join(CSRC, s) for s in DEVICE_SRCS], "-o", out]
+        _run(cmd)
+    return out
+
+
+def build_oracle(force=False):
+    odir = os.path.join(REPO, "oracle")
+    _run(["make", "-s", "-C", odir] + (["-B"] if force else []))
+    ref = os.environ.get("PNRT_REFERENCE", "/root/reference")
+    if os.path.isdir(os.path.join(ref, "include")):
+        _run(["make", "-s", "-C", os.path.join(odir, "ref"), f"REF={ref}"] + (["-B"] if force else []))
+
+
+def build_all(force=False):
+    build_host(force)
+    build_device(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,154 @@
+// pnraytracing_amd/csrc/pt_kernel.h -- the gfx950 radiance integrator.
+//
+// One lane per pixel; each lane runs all frames of a pnrt_render() call for its
+// pixel and blends them in order (ray_tracing.comp:988-991), so the RGBA32F
+// accumulation image is read once and written once per call instead of once
+// per frame.  The primary ray has no jitter (:980), so its closest hit is
+// traced once per call and reused by every frame.
+//
+// Bit-exactness rules (vs the CPU oracle, oracle/pn_oracle.c):
+//   * every float expression keeps the GLSL operation order; build with
+//     -ffp-contract=off (no FMA), IEEE division and sqrt, denormals kept;
+//   * BVH children are visited in the reference order (near child by the
+//     sign of dir[axis] first, :447-457) and a leaf's triangles in index
+//     order, so closest-hit ties resolve exactly as in BVHIntersect (:429-461);
+//   * RNG draws happen in the reference order (:880, :884, :561, :757, :643).
+#pragma once
+#include "pt_common.h"
+
+// ---- ray with per-ray precomputation ------------------------------------------------
+struct RayP {
+    f3 o, d;
+    f3 inv;           // 1/dir (BoundIntersect :214); also the triangle test's invDz
+    int kx, ky, kz;   // triangle-test axis permutation (:269-282)
+    float sx, sy, invDz;
+    bool cull_ok;     // z-slab culling is provably result-neutral for this ray
+};
+
+PN_DEV RayP make_ray(f3 o, f3 d, int mode) {
+    RayP r;
+    r.o = o; r.d = d;
+    r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.kx = 0; r.ky = 1; r.kz = 2;
+    if (d.z == 0.0f) {
+        if (pnm_fabs(d.x) > pnm_fabs(d.y)) { r.kx = 2; r.kz = 0; }
+        else { r.ky = 2; r.kz = 1; }
+    }
+    float dz = comp(d, r.kz);
+    r.sx = comp(d, r.kx); r.sy = comp(d, r.ky);
+    r.invDz = 1.0f / dz;
+    // z-slab culling needs finite rays and a non-tiny z so no sheared
+    // coordinate can overflow into NaN edge functions (Culling).
+    bool fin = pnm_fabs(o.x) < 1e6f && pnm_fabs(o.y) < 1e6f && pnm_fabs(o.z) < 1e6f &&
+               pnm_fabs(d.x) < 1e6f && pnm_fabs(d.y) < 1e6f && pnm_fabs(d.z) < 1e6f;
+    r.cull_ok = (mode != 0) && fin && pnm_fabs(dz) >= 1e-12f;
+    return r;
+}
+
+// BoundIntersect (:213-228) on one box, plus the box's z-slab interval in the
+// triangle test's frame (zlo, zhi) for culling.
+PN_DEV bool box_test(const RayP& r, float mnx, float mny, float mnz, float mxx, float mxy,
+                     float mxz, float& zlo, float& zhi) {
+    float fx = (mxx - r.o.x) * r.inv.x, fy = (mxy - r.o.y) * r.inv.y, fz = (mxz - r.o.z) * r.inv.z;
+    float nx = (mnx - r.o.x) * r.inv.x, ny = (mny - r.o.y) * r.inv.y, nz = (mnz - r.o.z) * r.inv.z;
+    float tmaxx = fmax_(fx, nx), tmaxy = fmax_(fy, ny), tmaxz = fmax_(fz, nz);
+    float tminx = fmin_(fx, nx), tminy = fmin_(fy, ny), tminz = fmin_(fz, nz);
+    float t1 = fmin_(tmaxx, fmin_(tmaxy, tmaxz));
+    float t0 = fmax_(tminx, fmax_(tminy, tminz));
+    float zf = r.kz == 2 ? fz : (r.kz == 0 ? fx : fy);
+    float zn = r.kz == 2 ? nz : (r.kz == 0 ? nx : ny);
+    zlo = zn < zf ? zn : zf;   // NaN -> comparisons below fail -> never culled
+    zhi = zn < zf ? zf : zn;
+    return t1 >= t0;
+}
+
+// Culling predicate: every triangle inside a box with this z-slab is rejected by
+// the watertight test at the current tMax (proof in DESIGN.md, "Culling").
+PN_DEV bool zcull(const RayP& r, float zlo, float zhi, float tmax_c) {
+    return r.cull_ok && (zhi <= 0.0f || (zlo > tmax_c && zlo > 1e-20f));
+}
+
+// Watertight triangle test front half (:254-318 / :360-424).
+PN_DEV bool tri_test(const RayP& r, const float4& t0, const float4& t1, const float4& t2,
+                     float tMax, float& e0o, float& e1o, float& e2o, float& deto, float& tso) {
+    f3 p0 = mk3(t0.x, t0.y, t0.z), p1 = mk3(t0.w, t1.x, t1.y), p2 = mk3(t1.z, t1.w, t2.x);
+    f3 P0 = sub(p0, r.o), P1 = sub(p1, r.o), P2 = sub(p2, r.o);
+    float P0x = comp(P0, r.kx), P0y = comp(P0, r.ky), P0z = comp(P0, r.kz);
+    float P1x = comp(P1, r.kx), P1y = comp(P1, r.ky), P1z = comp(P1, r.kz);
+    float P2x = comp(P2, r.kx), P2y = comp(P2, r.ky), P2z = comp(P2, r.kz);
+    P0x = P0x - (P0z * r.sx) * r.invDz; P0y = P0y - (P0z * r.sy) * r.invDz; P0z = P0z * r.invDz;
+    P1x = P1x - (P1z * r.sx) * r.invDz; P1y = P1y - (P1z * r.sy) * r.invDz; P1z = P1z * r.invDz;
+    P2x = P2x - (P2z * r.sx) * r.invDz; P2y = P2y - (P2z * r.sy) * r.invDz; P2z = P2z * r.invDz;
+    float e0 = P1x * P2y - P1y * P2x;
+    float e1 = P2x * P0y - P2y * P0x;
+    float e2 = P0x * P1y - P0y * P1x;
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    float det = (e0 + e1) + e2;
+    if (det == 0) return false;
+    float tScaled = (e0 * P0z + e1 * P1z) + e2 * P2z;
+    if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    e0o = e0; e1o = e1; e2o = e2; deto = det; tso = tScaled;
+    return true;
+}
+
+// BVHIntersect (ANY = false, returns the last accepted triangle) and
+// BVHIntersectP (ANY = true).  Reference visit order, stack of far children.
+template <bool ANY>
+PN_DEV bool traverse(const DevScene& s, const RayP& r, float& tMax, int& hitTri) {
+    float zlo, zhi;
+    if (!box_test(r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                  s.root_max[2], zlo, zhi))
+        return false;
+    int stackRef[PT_STACK];
+    int stackCnt[PT_STACK];
+    float stackZ[PT_STACK];
+    int sp = 0;
+    int ref = s.root_ref, cnt = s.root_cnt;
+    bool hit = false;
+    const float cullScale = 1.000001f;
+    for (;;) {
+        if (cnt == 0 && ref >= 0) {
+            const float4* n = s.nodes + 4 * (size_t)ref;
+            float4 a = n[0], b = n[1], c = n[2];
+            int4 m = *reinterpret_cast<const int4*>(n + 3);
+            float tmc = tMax * cullScale;
+            float zloL, zhiL, zloR, zhiR;
+            bool hL = box_test(r, a.x, a.y, a.z, a.w, b.x, b.y, zloL, zhiL);
+            bool hR = box_test(r, b.z, b.w, c.x, c.y, c.z, c.w, zloR, zhiR);
+            if (hL && zcull(r, zloL, zhiL, tmc)) hL = false;
+            if (hR && zcull(r, zloR, zhiR, tmc)) hR = false;
+            int axis = (int)((uint32_t)m.z >> 30);
+            int cntL = m.z & 0x3fffffff;
+            bool rightFirst = comp(r.d, axis) < 0;       // :448
+            int nearRef = rightFirst ? m.y : m.x, nearCnt = rightFirst ? m.w : cntL;
+            int farRef = rightFirst ? m.x : m.y, farCnt = rightFirst ? cntL : m.w;
+            bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+            float zFar = rightFirst ? zloL : zloR;
+            if (hNear) {
+                if (hFar) { stackRef[sp] = farRef; stackCnt[sp] = farCnt; stackZ[sp] = zFar; ++sp; }
+                ref = nearRef; cnt = nearCnt;
+                continue;
+            }
+            if (hFar) { ref = farRef; cnt = farCnt; continue; }
+        } else if (cnt > 0) {
+            for (int i = ref; i < ref + cnt; ++i) {
+                const float4* t = s.tris + 3 * (size_t)i;
+                float e0, e1, e2, det, ts;
+                if (tri_test(r, t[0], t[1], t[2], tMax, e0, e1, e2, det, ts)) {
+                    if (ANY) return true;
+                    tMax = ts * (1.0f / det);
+                    hitTri = i;
+                    hit = true;
+                }
+            }
+        }
+        // pop (far children re-checked against the tMax found meanwhile)
+        for (;;) {
+            if (sp == 0) return hit;
+            --sp;
+            ref = stackRef[sp]; cnt = stackCnt[sp];
+            if (!(r.cull_ok && stackZ[sp] > tMax * cullScale && stackZ[sp] > 1e-20f)) break;
+        }
+    }
+}

@@ -1,0 +1,205 @@
+// pnraytracing_amd/csrc/pt_shade.h -- shading side of the integrator:
+// materials, textures, environment, Disney BRDF and its sampling, restated
+// from shaders/ray_tracing.comp in its exact operation order.
+#pragma once
+#include "pt_kernel.h"
+
+struct Material {
+    f3 emssive, baseColor;
+    float subsurface, metallic, specular, specularTint, roughness, anisotropic;
+    float sheen, sheenTint, clearcoat, clearcoatGloss;
+};
+
+// GetMaterial (:122-144); the reference reads clearcoatGloss from param3[0]
+// (= sheen), not param4 (:139-142) -- kept.  Out-of-range ids read zeros.
+PN_DEV Material get_material(const DevScene& s, int i) {
+    Material m;
+    if (i < 0 || i >= s.n_materials) {
+        m.emssive = m.baseColor = mk3(0.f, 0.f, 0.f);
+        m.subsurface = m.metallic = m.specular = m.specularTint = m.roughness = m.anisotropic = 0.f;
+        m.sheen = m.sheenTint = m.clearcoat = m.clearcoatGloss = 0.f;
+        return m;
+    }
+    const float* p = s.materials + 18 * (size_t)i;
+    m.emssive = mk3(p[0], p[1], p[2]);
+    m.baseColor = mk3(p[3], p[4], p[5]);
+    m.subsurface = p[6]; m.metallic = p[7]; m.specular = p[8];
+    m.specularTint = p[9]; m.roughness = p[10]; m.anisotropic = p[11];
+    m.sheen = p[12]; m.sheenTint = p[13]; m.clearcoat = p[14];
+    m.clearcoatGloss = p[12];
+    return m;
+}
+PN_DEV f3 get_emissive(const DevScene& s, int i) {
+    if (i < 0 || i >= s.n_materials) return mk3(0.f, 0.f, 0.f);
+    const float* p = s.materials + 18 * (size_t)i;
+    return mk3(p[0], p[1], p[2]);
+}
+
+// ---- texture filtering: GL 4.5 8.14.2 LINEAR, level 0 (same formula as oracle) ----
+PN_DEV int wrap_clamp(float fl, int n) {
+    if (fl != fl) return 0;
+    fl = fmin_(fmax_(fl, -1.0f), (float)n);
+    int i = (int)fl;
+    return i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+}
+PN_DEV int wrap_repeat(float fl, int n) {
+    if (fl != fl) return 0;
+    float q = floorf(fl / (float)n);
+    float m = fl - (float)n * q;
+    m = fmin_(fmax_(m, 0.0f), (float)n);
+    int i = (int)m;
+    if (i >= n) i -= n;
+    if (i < 0) i += n;
+    return i;
+}
+PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
+    float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
+    float flu = floorf(fu), flv = floorf(fv);
+    float a = fu - flu, b = fv - flv;
+    int i0 = wrap_clamp(flu, w), i1 = wrap_clamp(flu + 1.0f, w);
+    int j0 = wrap_clamp(flv, h), j1 = wrap_clamp(flv + 1.0f, h);
+    float4 t00 = img[(size_t)j0 * w + i0], t10 = img[(size_t)j0 * w + i1];
+    float4 t01 = img[(size_t)j1 * w + i0], t11 = img[(size_t)j1 * w + i1];
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    return mk3(((w00 * t00.x + w10 * t10.x) + w01 * t01.x) + w11 * t11.x,
+               ((w00 * t00.y + w10 * t10.y) + w01 * t01.y) + w11 * t11.y,
+               ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);
+}
+PN_DEV f3 texel_u8(const DevScene& s, uint32_t px) {
+    return mk3(s.unorm8[px & 0xffu], s.unorm8[(px >> 8) & 0xffu], s.unorm8[(px >> 16) & 0xffu]);
+}
+// texture(textures[t], uv).rgb (:871): REPEAT, LINEAR at level 0; unbound -> 0
+PN_DEV f3 sample_albedo(const DevScene& s, int t, float u, float v) {
+    if (t < 0 || t >= s.n_tex || s.tex[t] == nullptr) return mk3(0.f, 0.f, 0.f);
+    int w = s.tex_w[t], h = s.tex_h[t];
+    const uint32_t* img = s.tex[t];
+    float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
+    float flu = floorf(fu), flv = floorf(fv);
+    float a = fu - flu, b = fv - flv;
+    int i0 = wrap_repeat(flu, w), i1 = wrap_repeat(flu + 1.0f, w);
+    int j0 = wrap_repeat(flv, h), j1 = wrap_repeat(flv + 1.0f, h);
+    f3 t00 = texel_u8(s, img[(size_t)j0 * w + i0]), t10 = texel_u8(s, img[(size_t)j0 * w + i1]);
+    f3 t01 = texel_u8(s, img[(size_t)j1 * w + i0]), t11 = texel_u8(s, img[(size_t)j1 * w + i1]);
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    return mk3(((w00 * t00.x + w10 * t10.x) + w01 * t01.x) + w11 * t11.x,
+               ((w00 * t00.y + w10 * t10.y) + w01 * t01.y) + w11 * t11.y,
+               ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);
+}
+
+// GetHDRImageColor (:181-193), invAtan = (0.1591, 0.3183) as written
+PN_DEV f3 env_color(const DevScene& s, f3 v) {
+    if (!s.has_hdr) return mk3(0.f, 0.f, 0.f);
+    float u = pnm_atan2(v.z, v.x), w = pnm_asin(v.y);
+    u = u * 0.1591f; w = w * 0.3183f;
+    u = u + 0.5f; w = w + 0.5f;
+    w = 1.0f - w;
+    return sample_clamp(s.hdr, s.hdr_w, s.hdr_h, u, w);
+}
+
+// SampleHDRImage (:560-576); r1, r2 drawn by the caller in order
+PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
+    f3 param = sample_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
+    param.y = 1.0f - param.y;
+    float phi = (2.0f * PT_PI) * (param.x - 0.5f);
+    float theta = PT_PI * (param.y - 0.5f);
+    float st, ct, sp, cp;
+    pnm_sincos(theta, st, ct);
+    pnm_sincos(phi, sp, cp);
+    L = mk3(ct * cp, st, ct * sp);
+    pdf = param.z;
+    float sinTheta = fmax_(1e-10f, st);
+    float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
+    pdf = pdf * convert;
+    return sample_clamp(s.hdr, s.hdr_w, s.hdr_h, param.x, param.y);
+}
+
+// ---- Disney BRDF (:649-849) -------------------------------------------------------
+PN_DEV float schlick(float u) {
+    float m = clampf(1.0f - u, 0.0f, 1.0f);
+    float m2 = m * m;
+    return (m2 * m2) * m;
+}
+PN_DEV float gtr1(float NdotH, float a) {
+    if (a >= 1) return 1.0f / PT_PI;
+    float a2 = a * a;
+    float t = 1.0f + ((a2 - 1.0f) * NdotH) * NdotH;
+    return (a2 - 1.0f) / ((PT_PI * pnm_log(a2)) * t);
+}
+PN_DEV float gtr2(float NdotH, float a) {
+    float a2 = a * a;
+    float t = 1.0f + ((a2 - 1.0f) * NdotH) * NdotH;
+    return a2 / ((PT_PI * t) * t);
+}
+PN_DEV float gtr2_aniso(float NdotH, float HdotX, float HdotY, float ax, float ay) {
+    return 1.0f / (((PT_PI * ax) * ay) * sqr((sqr(HdotX / ax) + sqr(HdotY / ay)) + NdotH * NdotH));
+}
+PN_DEV float smithG(float NdotV, float alphaG) {
+    float a = alphaG * alphaG;
+    float b = NdotV * NdotV;
+    return 1.0f / (NdotV + sqrtf((a + b) - a * b));
+}
+PN_DEV float smithG_aniso(float NdotV, float VdotX, float VdotY, float ax, float ay) {
+    return 1.0f / (NdotV + sqrtf((sqr(VdotX * ax) + sqr(VdotY * ay)) + sqr(NdotV)));
+}
+
+// Everything DisneyBRDF computes from (V, N, X, Y, material) alone, evaluated
+// once per bounce and shared by its three calls -- the same float ops as
+// recomputing them per call, so the results are bit-identical.
+struct BrdfCtx {
+    f3 V, N, X, Y;
+    float NdotV;
+    f3 Cdlin, Cspec0, Csheen;
+    float FV, ax, ay, GsV, GrV, alphaDr;
+    float rough, subsurface, metallic, sheen, clearcoat;
+};
+PN_DEV BrdfCtx brdf_prepare(f3 V, f3 N, f3 X, f3 Y, const Material& m) {
+    BrdfCtx b;
+    b.V = V; b.N = N; b.X = X; b.Y = Y;
+    b.NdotV = dot(N, V);
+    b.Cdlin = m.baseColor;
+    float Cdlum = (0.3f * b.Cdlin.x + 0.6f * b.Cdlin.y) + 0.1f * b.Cdlin.z;
+    f3 Ctint = (Cdlum > 0) ? divs(b.Cdlin, Cdlum) : mk3(1.f, 1.f, 1.f);
+    f3 Cspec = smul(m.specular, mixv(mk3(1.f, 1.f, 1.f), Ctint, m.specularTint));
+    b.Cspec0 = mixv(smul(0.08f, Cspec), b.Cdlin, m.metallic);
+    b.Csheen = mixv(mk3(1.f, 1.f, 1.f), Ctint, m.sheenTint);
+    b.FV = schlick(b.NdotV);
+    float aspect = sqrtf(1.0f - m.anisotropic * 0.9f);
+    b.ax = fmax_(0.001f, sqr(m.roughness) / aspect);
+    b.ay = fmax_(0.001f, sqr(m.roughness) * aspect);
+    b.GsV = smithG_aniso(b.NdotV, dot(V, X), dot(V, Y), b.ax, b.ay);
+    b.GrV = smithG(b.NdotV, 0.25f);
+    b.alphaDr = mixf(0.1f, 0.001f, m.clearcoatGloss);
+    b.rough = m.roughness; b.subsurface = m.subsurface; b.metallic = m.metallic;
+    b.sheen = m.sheen; b.clearcoat = m.clearcoat;
+    return b;
+}
+// DisneyBRDF (:788-849)
+PN_DEV f3 disney(const BrdfCtx& b, f3 L) {
+    float NdotL = dot(b.N, L), NdotV = b.NdotV;
+    if (NdotL < 0 || NdotV < 0) return mk3(0.f, 0.f, 0.f);
+    f3 H = normalize(add(L, b.V));
+    float NdotH = dot(b.N, H), LdotH = dot(L, H);
+    float Fd90 = 0.5f + ((2.0f * LdotH) * LdotH) * b.rough;
+    float FL = schlick(NdotL), FV = b.FV;
+    float Fd = mixf(1.0f, Fd90, FL) * mixf(1.0f, Fd90, FV);
+    float Fss90 = (LdotH * LdotH) * b.rough;
+    float Fss = mixf(1.0f, Fss90, FL) * mixf(1.0f, Fss90, FV);
+    float ss = 1.25f * (Fss * (1.0f / (NdotL + NdotV) - 0.5f) + 0.5f);
+    float Ds = gtr2_aniso(NdotH, dot(H, b.X), dot(H, b.Y), b.ax, b.ay);
+    float FH = schlick(LdotH);
+    f3 Fs = mixv(b.Cspec0, mk3(1.f, 1.f, 1.f), FH);
+    float Gs = smithG_aniso(NdotL, dot(L, b.X), dot(L, b.Y), b.ax, b.ay);
+    Gs = Gs * b.GsV;
+    float Dr = gtr1(NdotH, b.alphaDr);
+    float Fr = mixf(0.04f, 1.0f, FH);
+    float Gr = smithG(NdotL, 0.25f) * b.GrV;
+    f3 Fsheen = smul(FH * b.sheen, b.Csheen);
+    f3 diffuse = add(smul((1.0f / PT_PI) * mixf(Fd, ss, b.subsurface), b.Cdlin), Fsheen);
+    f3 specular = muls(smul(Gs, Fs), Ds);
+    float cc = (((0.25f * Gr) * Fr) * Dr) * b.clearcoat;
+    return add(add(muls(diffuse, 1.0f - b.metallic), specular), mk3(cc, cc, cc));
+}
+
+PN_DEV f3 tangent_to_world(f3 t, f3 b, f3 n, f3 v) {
+    return add(add(smul(v.x, t), smul(v.y, b)), smul(v.z, n));
+}

@@ -1,0 +1,40 @@
+"""The C-ABI libraries load and export every symbol their headers declare
+(no compute calls: runs without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from pnraytracing_amd import _native as N
+
+INC = os.path.join(os.path.dirname(os.path.dirname(__file__)), "include")
+
+
+def declared(header):
+    src = open(os.path.join(INC, header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pnrt_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.mark.parametrize("header,path", [("pnrt.h", N.DEVICE_LIB), ("pnrt_host.h", N.HOST_LIB)])
+def test_library_exports_declared_symbols(header, path):
+    lib = ctypes.CDLL(path)
+    names = declared(header)
+    assert len(names) >= 10
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_device_library_typed_and_versioned():
+    lib = N.device_lib()
+    assert b"gfx950" in lib.pnrt_version()
+
+
+def test_device_create_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from pnraytracing_amd.tracer import PathTracer, PnrtError
+    with pytest.raises(PnrtError):
+        PathTracer(0)
