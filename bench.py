@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=["C2", "C4", "C5"])
     ap.add_argument("--mode", default="zcull", choices=["exact", "zcull"])
+    ap.add_argument("--kernel", default="v2", choices=["v1", "v2"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-image", default="")
@@ -57,23 +58,24 @@ def cpu_baseline(cfg, target_s: float):
     threads = max(1, min(threads, 64))
     o = pyoracle.Oracle(cfg)
     H = cfg.height
-    # calibrate on a few rows, then size the sample to ~target_s
+    # whole-frame 4-spp iterations of the same workload until ~target_s (max 8)
+    acc = np.zeros((H, cfg.width, 4), np.float32)
+    tot = None
+    it = 0
     t = time.perf_counter()
-    _, st = o.render(0, cfg.spp, rows=(H // 2, H), y_step=H // 2 // max(1, threads), threads=threads)
-    dt = max(time.perf_counter() - t, 1e-3)
-    rows_cal = len(range(H // 2, H, H // 2 // max(1, threads)))
-    rows = int(np.clip(rows_cal * target_s / dt, threads, H))
-    step = max(1, H // rows)
-    t = time.perf_counter()
-    _, st = o.render(0, cfg.spp, rows=(step // 2, H), y_step=step, threads=threads)
+    while it < 8:
+        _, st = o.render(it * cfg.spp, cfg.spp, accum=acc, threads=threads)
+        tot = st if tot is None else {k: tot[k] + st[k] for k in st}
+        it += 1
+        if time.perf_counter() - t >= target_s:
+            break
     dt = time.perf_counter() - t
-    n = st["samples"]
-    bps = pyoracle.algorithmic_bytes(st) / n
-    nrows = len(range(step // 2, H, step))
+    n = tot["samples"]
+    bps = pyoracle.algorithmic_bytes(tot) / n
     return ({"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-             "sample": f"{cfg.name}: {nrows} rows (every {step}th) x {cfg.width} px x {cfg.spp} spp = {n} samples "
+             "sample": f"{cfg.name}: {it} full {cfg.width}x{H} iterations x {cfg.spp} spp = {n} samples "
                        f"in {dt:.1f}s, oracle/pn_oracle.c OpenMP {threads} threads"},
-            bps, st)
+            bps, tot)
 
 
 def main():
@@ -91,16 +93,18 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from pnraytracing_amd import scenes
-    from pnraytracing_amd.tracer import TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, shard_rows
+    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, shard_rows
 
     builders = {"C2": scenes.bunny_c2, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
     cfg = builders[args.config]()
     W, H, spp = cfg.width, cfg.height, cfg.spp
 
     pt = PathTracer(local)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()               # a real stream handle (the default one is NULL)
+    torch.cuda.set_stream(stream)
     pt.set_stream(stream.cuda_stream)
-    pt.load(cfg, TRAVERSE_ZCULL if args.mode == "zcull" else TRAVERSE_EXACT)
+    opts = (TRAVERSE_ZCULL if args.mode == "zcull" else TRAVERSE_EXACT) | (KERNEL_V1 if args.kernel == "v1" else 0)
+    pt.load(cfg, opts)
     info = pt.device_info()
 
     rows = [torch.as_tensor(shard_rows(H, BAND, world, r), device="cuda") for r in range(world)]
@@ -176,8 +180,8 @@ def main():
             "data": "synthetic (procedural bunny stand-in, reference 1k HDR)",
             "config": {"workload": f"{cfg.name}: {cfg.description}", "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
-                       "traverse": args.mode, "parallelism": f"row-bands{BAND}x{world}",
-                       "kernel": "pt_render_kernel"},
+                       "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
+                       "kernel": "pt_wave_kernel" if args.kernel == "v2" else "pt_render_kernel"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

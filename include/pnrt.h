@@ -45,9 +45,10 @@ typedef struct {
     int stack_limit;     /* traversal stack entries available per lane       */
 } pnrt_device_info;
 
-/* Traversal options (pnrt_set_options). */
+/* Options (pnrt_set_options): a traversal mode, optionally | PNRT_KERNEL_V1. */
 #define PNRT_TRAVERSE_EXACT 0   /* the reference's box visits (no tMax culling)      */
 #define PNRT_TRAVERSE_ZCULL 1   /* + provably result-neutral z-slab culling (default) */
+#define PNRT_KERNEL_V1 0x100    /* one-lane-per-pixel kernel (A/B baseline); default: persistent wave kernel */
 
 const char* pnrt_version(void);
 
@@ -90,7 +91,7 @@ int pnrt_upload_env(pnrt_ctx* ctx, const float* hdr_rgb, const float* random_hdr
 int pnrt_set_frame(pnrt_ctx* ctx, int width, int height, const pnrt_camera* camera,
                    int max_bounce_depth);
 
-int pnrt_set_options(pnrt_ctx* ctx, int traverse_mode);
+int pnrt_set_options(pnrt_ctx* ctx, int options);
 
 /* Replaces glDispatchCompute (main.cpp:613) called once per frame for frames
  * first_frame .. first_frame + n_frames - 1 (frameCount uniform), blended in

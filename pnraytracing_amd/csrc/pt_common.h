@@ -24,14 +24,21 @@
 //   n0 = (L.min.x, L.min.y, L.min.z, L.max.x)
 //   n1 = (L.max.y, L.max.z, R.min.x, R.min.y)
 //   n2 = (R.min.z, R.max.x, R.max.y, R.max.z)
-//   n3 = (refL, refR, cntL | axis << 30, cntR)      (ints)
-// child ref: cnt > 0 -> leaf, triangles [ref, ref + cnt); cnt == 0 -> interior
-// node index ref (ref < 0: empty).  Boxes are the reference floats bit for bit.
+//   n3 = (refL, refR, axis, 0)                      (uints)
+// child ref (32 bits): interior = node index; leaf = REF_LEAF | [29:7] first
+// triangle | [6:0] count, or REF_LEAF | REF_TABLE | index into leaf_table
+// (int2 start, count) when the range does not fit; REF_LEAF alone = empty.
+// Boxes are the reference floats bit for bit.
 // Triangle (BVH order), 48 B: t0 = (p0.xyz, p1.x), t1 = (p1.yz, p2.xy),
 //   t2 = (p2.z, matId, texId, -) ; tri_idx = (i0, i1, i2, -)
 // Vertex 32 B: v0 = (pos.xyz, n.x), v1 = (n.yz, u, v)
+#define REF_LEAF 0x80000000u
+#define REF_TABLE 0x40000000u
+#define REF_NONE 0xFFFFFFFFu
+
 struct DevScene {
     const float4* nodes;
+    const int2* leaf_table;
     const float4* tris;
     const int4* tri_idx;
     const float4* verts;
@@ -40,7 +47,7 @@ struct DevScene {
     int n_nodes, n_tris, n_verts, n_materials, n_lights;
     float lights_sum_area;
     float root_min[3], root_max[3];
-    int root_ref, root_cnt;
+    uint32_t root_ref;
     int has_hdr, hdr_w, hdr_h;
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad

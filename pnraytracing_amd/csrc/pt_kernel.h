@@ -92,47 +92,56 @@ PN_DEV bool tri_test(const RayP& r, const float4& t0, const float4& t1, const fl
     return true;
 }
 
+PN_DEV void decode_leaf(const DevScene& s, uint32_t ref, int& start, int& cnt) {
+    if (ref & REF_TABLE) {
+        int2 e = s.leaf_table[ref & 0x3fffffffu];
+        start = e.x; cnt = e.y;
+    } else {
+        start = (int)((ref >> 7) & 0x7fffffu);
+        cnt = (int)(ref & 0x7fu);
+    }
+}
+
 // BVHIntersect (ANY = false, returns the last accepted triangle) and
-// BVHIntersectP (ANY = true).  Reference visit order, stack of far children.
+// BVHIntersectP (ANY = true): reference visit order, private stack of far
+// children (used by the one-ray-per-lane kernels: primary pass and v1).
 template <bool ANY>
 PN_DEV bool traverse(const DevScene& s, const RayP& r, float& tMax, int& hitTri) {
     float zlo, zhi;
     if (!box_test(r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
                   s.root_max[2], zlo, zhi))
         return false;
-    int stackRef[PT_STACK];
-    int stackCnt[PT_STACK];
+    uint32_t stackRef[PT_STACK];
     float stackZ[PT_STACK];
     int sp = 0;
-    int ref = s.root_ref, cnt = s.root_cnt;
+    uint32_t cur = s.root_ref;
     bool hit = false;
     const float cullScale = 1.000001f;
     for (;;) {
-        if (cnt == 0 && ref >= 0) {
-            const float4* n = s.nodes + 4 * (size_t)ref;
+        if (!(cur & REF_LEAF)) {
+            const float4* n = s.nodes + 4 * (size_t)cur;
             float4 a = n[0], b = n[1], c = n[2];
-            int4 m = *reinterpret_cast<const int4*>(n + 3);
+            uint4 m = *reinterpret_cast<const uint4*>(n + 3);
             float tmc = tMax * cullScale;
             float zloL, zhiL, zloR, zhiR;
             bool hL = box_test(r, a.x, a.y, a.z, a.w, b.x, b.y, zloL, zhiL);
             bool hR = box_test(r, b.z, b.w, c.x, c.y, c.z, c.w, zloR, zhiR);
             if (hL && zcull(r, zloL, zhiL, tmc)) hL = false;
             if (hR && zcull(r, zloR, zhiR, tmc)) hR = false;
-            int axis = (int)((uint32_t)m.z >> 30);
-            int cntL = m.z & 0x3fffffff;
-            bool rightFirst = comp(r.d, axis) < 0;       // :448
-            int nearRef = rightFirst ? m.y : m.x, nearCnt = rightFirst ? m.w : cntL;
-            int farRef = rightFirst ? m.x : m.y, farCnt = rightFirst ? cntL : m.w;
+            bool rightFirst = comp(r.d, (int)m.z) < 0;       // :448
+            uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
             bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
             float zFar = rightFirst ? zloL : zloR;
             if (hNear) {
-                if (hFar) { stackRef[sp] = farRef; stackCnt[sp] = farCnt; stackZ[sp] = zFar; ++sp; }
-                ref = nearRef; cnt = nearCnt;
+                if (hFar) { stackRef[sp] = farRef; stackZ[sp] = zFar; ++sp; }
+                cur = nearRef;
                 continue;
             }
-            if (hFar) { ref = farRef; cnt = farCnt; continue; }
-        } else if (cnt > 0) {
-            for (int i = ref; i < ref + cnt; ++i) {
+            if (hFar) { cur = farRef; continue; }
+        } else {
+            int start, cnt;
+            decode_leaf(s, cur, start, cnt);
+            for (int i = start; i < start + cnt; ++i) {
                 const float4* t = s.tris + 3 * (size_t)i;
                 float e0, e1, e2, det, ts;
                 if (tri_test(r, t[0], t[1], t[2], tMax, e0, e1, e2, det, ts)) {
@@ -147,7 +156,7 @@ PN_DEV bool traverse(const DevScene& s, const RayP& r, float& tMax, int& hitTri)
         for (;;) {
             if (sp == 0) return hit;
             --sp;
-            ref = stackRef[sp]; cnt = stackCnt[sp];
+            cur = stackRef[sp];
             if (!(r.cull_ok && stackZ[sp] > tMax * cullScale && stackZ[sp] > 1e-20f)) break;
         }
     }

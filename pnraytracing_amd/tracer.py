@@ -16,6 +16,7 @@ from .host import PackedScene
 
 TRAVERSE_EXACT = 0
 TRAVERSE_ZCULL = 1
+KERNEL_V1 = 0x100      # | with a traverse mode: the one-lane-per-pixel A/B baseline kernel
 
 
 class PnrtError(RuntimeError):

@@ -11,7 +11,7 @@ import pytest
 
 import pyoracle
 from pnraytracing_amd import scenes as S
-from pnraytracing_amd.tracer import TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, PnrtError
+from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, PnrtError
 
 pytestmark = pytest.mark.gpu
 
@@ -82,8 +82,8 @@ def test_math_bitwise(pt, fn):
 
 
 # ---- whole images ---------------------------------------------------------------------------
-@pytest.mark.parametrize("mode", [TRAVERSE_EXACT, TRAVERSE_ZCULL])
-@pytest.mark.parametrize("first,n", [(0, 1), (0, 4), (7, 3)])
+@pytest.mark.parametrize("mode", [TRAVERSE_EXACT, TRAVERSE_ZCULL, TRAVERSE_ZCULL | KERNEL_V1])
+@pytest.mark.parametrize("first,n", [(0, 1), (0, 4), (7, 3), (0, 11)])
 def test_c1_bitwise(pt, mode, first, n):
     c = cfg("C1")
     got = gpu_render(pt, c, first, n, mode)
@@ -101,9 +101,10 @@ def test_c1_depth_variants(pt):
         assert_bitwise(got, ref, f"C1 depth {depth}")
 
 
-def test_c2_small_bitwise(pt):
+@pytest.mark.parametrize("mode", [TRAVERSE_ZCULL, TRAVERSE_ZCULL | KERNEL_V1])
+def test_c2_small_bitwise(pt, mode):
     c = cfg("C2", width=192, height=108, spp=4)
-    got = gpu_render(pt, c, 0, 4)
+    got = gpu_render(pt, c, 0, 4, mode)
     ref, _ = pyoracle.Oracle(c).render(0, 4)
     assert_bitwise(got, ref, "C2 192x108")
 
@@ -132,12 +133,14 @@ def test_c4_rows_bitwise(pt):
 
 # ---- size-independent properties at full size ------------------------------------------------
 def test_traversal_modes_agree_fullsize(pt):
-    """z-slab culling is result-neutral: exact and culled traversals agree on
-    every pixel of the 1080p bench image (8.3M samples)."""
+    """z-slab culling is result-neutral and both kernels compute the same
+    image: every pixel of the 1080p bench image (8.3M samples)."""
     c = cfg("C2")
     a = gpu_render(pt, c, 0, 4, TRAVERSE_EXACT)
     b = gpu_render(pt, c, 0, 4, TRAVERSE_ZCULL)
     assert_bitwise(b, a, "exact vs zcull")
+    v1 = gpu_render(pt, c, 0, 4, TRAVERSE_ZCULL | KERNEL_V1)
+    assert_bitwise(v1, a, "v1 vs v2")
 
 
 def test_progressive_split_calls(pt):
