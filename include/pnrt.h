@@ -45,10 +45,12 @@ typedef struct {
     int stack_limit;     /* traversal stack entries available per lane       */
 } pnrt_device_info;
 
-/* Options (pnrt_set_options): a traversal mode, optionally | PNRT_KERNEL_V1. */
+/* Options (pnrt_set_options): a traversal mode, optionally | a kernel variant. */
 #define PNRT_TRAVERSE_EXACT 0   /* the reference's box visits (no tMax culling)      */
 #define PNRT_TRAVERSE_ZCULL 1   /* + provably result-neutral z-slab culling (default) */
-#define PNRT_KERNEL_V1 0x100    /* one-lane-per-pixel kernel (A/B baseline); default: persistent wave kernel */
+#define PNRT_KERNEL_V1 0x100    /* A/B baseline: one lane per pixel, frames in-lane        */
+#define PNRT_KERNEL_V2 0x200    /* A/B baseline: persistent state-machine megakernel       */
+                                /* default: wavefront (setup / trace / shade per bounce)   */
 
 const char* pnrt_version(void);
 

@@ -16,6 +16,7 @@
 
 #include "pt_path.h"
 #include "pt_wave.h"
+#include "pt_wf.h"
 
 __global__ void pt_pack_rows_kernel(const float4* accum, float4* dst, int width, int rows, int band,
                                     int n_shards, int shard) {
@@ -75,13 +76,17 @@ struct pnrt_ctx {
     bool has_frame = false;
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
-    int kernel = 2;                        // 2 = persistent wave kernel, 1 = v1
+    int kernel = 3;                        // 3 = wavefront (default), 2 = persistent megakernel, 1 = v1
     // v2 work buffers (grown on demand)
     float4* primary = nullptr;  size_t primary_cap = 0;
     float4* colors = nullptr;   size_t colors_cap = 0;
     uint2* ovf = nullptr;       size_t ovf_cap = 0;
     unsigned int* counter = nullptr;
     int wave_grid = 0;
+    // v3 wavefront buffers
+    void* wf = nullptr;         size_t wf_cap = 0;
+    uint2* wf_ovf = nullptr;    size_t wf_ovf_cap = 0;
+    int trace_grid = 0;
 };
 
 static int set_err(pnrt_ctx* c, int code, const std::string& m) {
@@ -129,6 +134,61 @@ static int upload(pnrt_ctx* c, const std::vector<T>& v, const T** out) {
 
 static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 
+// v3 wavefront: primary pass, then per frame chunk gen -> {setup, trace, shade}
+// x max_depth -> ordered blend.
+static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
+    const size_t pix = (size_t)fp.rows * c->width;
+    const uint32_t chunk = nf < PTW_MAX_CHUNK_FRAMES ? nf : PTW_MAX_CHUNK_FRAMES;
+    const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
+    const size_t nmax = (size_t)tiles_x * tiles_y * 64 * chunk;
+    if (c->trace_grid == 0) {
+        int per_cu = 0, cus = 0;
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace, WF_TRACE_BLOCK, 0));
+        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
+    }
+    const size_t per_path = 16 * 12 + 4 + 4 + 2;      // S0-5, C0-3, R0-1 | flags | hit | occ
+    int rc;
+    if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
+        (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
+        (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 1024)) ||
+        (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * WF_OVF * 8)))
+        return rc;
+    hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, s, fp,
+                       c->primary);
+    HIPCHK(c, hipGetLastError());
+    for (uint32_t f0 = 0; f0 < nf; f0 += chunk) {
+        uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
+        WfBufs b;
+        size_t n = (size_t)tiles_x * tiles_y * 64 * cf;
+        char* base = static_cast<char*>(c->wf);
+        float4** f4[] = {&b.S0, &b.S1, &b.S2, &b.S3, &b.S4, &b.S5, &b.C0, &b.C1, &b.C2, &b.C3, &b.R0, &b.R1};
+        size_t off = 0;
+        for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
+        b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
+        b.hit = reinterpret_cast<int*>(base + off); off += n * 4;
+        b.occ = reinterpret_cast<uint8_t*>(base + off); off += n * 2;
+        b.ovf = c->wf_ovf;
+        b.n = (uint32_t)n;
+        b.chunk_frames = (int)cf;
+        b.tiles_x = tiles_x;
+        b.first_frame = first + f0;
+        const dim3 g((unsigned)((n + 255) / 256));
+        hipLaunchKernelGGL(pt_wf_gen, g, dim3(256), 0, c->stream, fp, b, (const float4*)c->primary, c->colors);
+        HIPCHK(c, hipGetLastError());
+        for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
+            hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
+            hipLaunchKernelGGL(pt_wf_trace, dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            hipLaunchKernelGGL(pt_wf_shade, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
+            HIPCHK(c, hipGetLastError());
+        }
+        hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
+                           (const float4*)c->colors, c->accum, (int)cf, first + f0);
+        HIPCHK(c, hipGetLastError());
+    }
+    return PNRT_OK;
+}
+
 extern "C" {
 
 const char* pnrt_version(void) { return "pnrt-mi355x 0.1 (gfx950)"; }
@@ -172,6 +232,7 @@ void pnrt_destroy(pnrt_ctx* c) {
     (void)hipFree(c->unorm8);
     (void)hipFree(c->accum);
     (void)hipFree(c->primary); (void)hipFree(c->colors); (void)hipFree(c->ovf); (void)hipFree(c->counter);
+    (void)hipFree(c->wf); (void)hipFree(c->wf_ovf);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -187,10 +248,11 @@ int pnrt_set_stream(pnrt_ctx* c, void* s) {
 int pnrt_set_options(pnrt_ctx* c, int options) {
     if (!c) return PNRT_E_ARG;
     int mode = options & 0xff;
-    if ((mode != PNRT_TRAVERSE_EXACT && mode != PNRT_TRAVERSE_ZCULL) || (options & ~0x1ff))
+    if ((mode != PNRT_TRAVERSE_EXACT && mode != PNRT_TRAVERSE_ZCULL) || (options & ~0x3ff) ||
+        ((options & PNRT_KERNEL_V1) && (options & PNRT_KERNEL_V2)))
         return set_err(c, PNRT_E_ARG, "unknown option bits");
     c->mode = mode;
-    c->kernel = (options & PNRT_KERNEL_V1) ? 1 : 2;
+    c->kernel = (options & PNRT_KERNEL_V1) ? 1 : (options & PNRT_KERNEL_V2) ? 2 : 3;
     return PNRT_OK;
 }
 
@@ -418,6 +480,7 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
         HIPCHK(c, hipGetLastError());
         return PNRT_OK;
     }
+    if (c->kernel == 3) return render_wavefront(c, s, fp, first, nf);
     // ---- v2: primary pass, persistent megakernel per frame chunk, ordered blend
     if (!c->counter) HIPCHK(c, hipMalloc(&c->counter, 64));
     if (c->wave_grid == 0) {

@@ -1,0 +1,426 @@
+// pnraytracing_amd/csrc/pt_wf.h -- v3 integrator: wavefront path tracing for gfx950.
+//
+// All samples (pixel, frame) of a pnrt_render chunk are paths held in SoA
+// buffers in HBM.  Per bounce three kernels run over every path slot:
+//   setup  -- material, light/env/BSDF sampling in the reference RNG order, and
+//             every BRDF value the bounce needs (evaluated before the shadow
+//             tests: same float ops, same bits); emits up to three rays
+//   trace  -- ONE persistent traversal kernel for all rays of the bounce
+//             (light shadow, env shadow: any-hit; continuation: closest-hit),
+//             small register footprint -> high occupancy, LDS short stack
+//   shade  -- "MIS" accumulation with the occlusion results, the continuation
+//             hit (emission, throughput), next bounce or the final colour
+// so each kernel is compact and coherent instead of one 240-VGPR megakernel.
+#pragma once
+#include "pt_wave.h"
+
+#define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
+#define WF_OVF 56
+#define WF_TRACE_BLOCK 256
+
+// flags[path]: bit0 alive, bit1 light ray, bit2 env ray, bit3 continuation ray,
+// bits 8..10 bounce
+#define WF_ALIVE 1u
+#define WF_RLIGHT 2u
+#define WF_RENV 4u
+#define WF_RCONT 8u
+
+struct WfBufs {
+    // path state
+    float4* S0;   // P.xyz, u
+    float4* S1;   // N.xyz, v
+    float4* S2;   // Lo.xyz, bits(mat | (tex+1)<<24)
+    float4* S3;   // cw.xyz, bits(seed)
+    float4* S4;   // V.xyz, bits(sample id: lr*W + x | slot << 28... see wf_id)
+    float4* S5;   // base.xyz, -
+    uint32_t* flags;
+    // bounce candidates
+    float4* C0;   // LDirect.xyz, lightPDF
+    float4* C1;   // LEnvironment.xyz, enPDF
+    float4* C2;   // dBRDF.xyz, |N.L|
+    float4* C3;   // L.xyz, dPDF
+    float4* R0;   // light shadow direction (unnormalised), -
+    float4* R1;   // env shadow direction, -
+    // trace results
+    uint8_t* occ;      // [2 * n]: light, env occluded
+    int* hit;          // continuation hit triangle or -1
+    uint2* ovf;        // traversal stack spill
+    uint32_t n;        // path slots
+    int chunk_frames;
+    int tiles_x;
+    uint32_t first_frame;
+};
+
+// path slot -> (x, local row, frame slot): same tile order as the v2 kernel
+PN_DEV void wf_coords(const WfBufs& b, uint32_t s, int& x, int& lr, int& k) {
+    uint32_t per_tile = 64u * (uint32_t)b.chunk_frames;
+    uint32_t tile = s / per_tile, rem = s - tile * per_tile;
+    k = (int)(rem >> 6);
+    int p = (int)(rem & 63u);
+    int ty = (int)(tile / (uint32_t)b.tiles_x), tx = (int)(tile - (uint32_t)ty * b.tiles_x);
+    x = tx * 8 + (p & 7);
+    lr = ty * 8 + (p >> 3);
+}
+
+PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
+    color = mk3(clampf(color.x, 0.f, 1.f), clampf(color.y, 0.f, 1.f), clampf(color.z, 0.f, 1.f));
+    colors[((size_t)k * fp.rows + lr) * fp.width + x] = make_float4(color.x, color.y, color.z, 0.f);
+}
+
+// ---- gen: start every path from its pixel's primary hit --------------------------------------
+__global__ void __launch_bounds__(256) pt_wf_gen(FrameParams fp, WfBufs b, const float4* primary, float4* colors) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    int x, lr, k;
+    wf_coords(b, i, x, lr, k);
+    if (x >= fp.width || lr >= fp.rows) { b.flags[i] = 0; return; }
+    const float4* rec = primary + 3 * ((size_t)lr * fp.width + x);
+    float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+    int mt = __float_as_int(q0.w);
+    f3 base = mk3(q2.y, q2.z, q2.w);
+    if (mt == -1) { b.flags[i] = 0; wf_write_color(fp, colors, k, lr, x, base); return; }   // primary miss
+    if (fp.max_depth == 0) { b.flags[i] = 0; wf_write_color(fp, colors, k, lr, x, add(base, mk3(0.f, 0.f, 0.f))); return; }
+    int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+    uint32_t frame = b.first_frame + (uint32_t)k;
+    uint32_t seed = ((uint32_t)x * 1973u + (uint32_t)py * 9277u + frame * 26699u) | 1u;
+    f3 V = neg(camera_dir(fp, x, py));
+    b.S0[i] = make_float4(q0.x, q0.y, q0.z, q1.w);
+    b.S1[i] = make_float4(q1.x, q1.y, q1.z, q2.x);
+    b.S2[i] = make_float4(0.f, 0.f, 0.f, q0.w);
+    b.S3[i] = make_float4(1.f, 1.f, 1.f, __uint_as_float(seed));
+    b.S4[i] = make_float4(V.x, V.y, V.z, 0.f);
+    b.S5[i] = make_float4(base.x, base.y, base.z, 0.f);
+    b.flags[i] = WF_ALIVE;
+}
+
+// ---- setup: one bounce's sampling and BRDF values (ray_tracing.comp:866-934) -----------------
+__global__ void __launch_bounds__(256) pt_wf_setup(DevScene s, FrameParams fp, WfBufs b) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    uint32_t fl = b.flags[i];
+    if (!(fl & WF_ALIVE)) return;
+    const int bounce = (int)((fl >> 8) & 7u);
+    int x, lr, k;
+    wf_coords(b, i, x, lr, k);
+    const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+    const uint32_t frame = b.first_frame + (uint32_t)k;
+    float4 s0 = b.S0[i], s1 = b.S1[i], s2 = b.S2[i], s3 = b.S3[i], s4 = b.S4[i];
+    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z), V = mk3(s4.x, s4.y, s4.z);
+    int mt = __float_as_int(s2.w);
+    int hmat = mt & 0x00ffffff, htex = (int)((uint32_t)mt >> 24) - 1;
+    uint32_t seed = __float_as_uint(s3.w);
+
+    Material m = get_material(s, hmat);
+    if (htex != -1) m.baseColor = sample_albedo(s, htex, s0.w, s1.w);
+    f3 T, B;
+    if (N.z > 0.9999995f) T = mk3(1.f, 0.f, 0.f);
+    else T = normalize(cross(N, mk3(0.f, 0.f, 1.f)));
+    B = cross(N, T);
+    BrdfCtx bc = brdf_prepare(V, N, T, B, m);
+    uint32_t nfl = WF_ALIVE | ((uint32_t)bounce << 8);
+
+    // direct light (:878-909): candidate values, used if the shadow ray is unoccluded
+    f3 LD = mk3(0.f, 0.f, 0.f);
+    float pl = 0.f;
+    int triIndex = light_index(s, rand01(seed));
+    if (triIndex != -1) {
+        float u0 = rand01(seed), u1 = rand01(seed);
+        int4 id = s.tri_idx[triIndex];
+        float4 va0 = s.verts[2 * (size_t)id.x], vb0 = s.verts[2 * (size_t)id.x + 1];
+        float4 va1 = s.verts[2 * (size_t)id.y], vb1 = s.verts[2 * (size_t)id.y + 1];
+        float4 va2 = s.verts[2 * (size_t)id.z], vb2 = s.verts[2 * (size_t)id.z + 1];
+        float su0 = sqrtf(u0);
+        float bx = 1.0f - su0, by = u1 * su0, bz = (1.0f - bx) - by;
+        f3 p0 = mk3(va0.x, va0.y, va0.z), p1 = mk3(va1.x, va1.y, va1.z), p2 = mk3(va2.x, va2.y, va2.z);
+        f3 n0 = mk3(va0.w, vb0.x, vb0.y), n1 = mk3(va1.w, vb1.x, vb1.y), n2 = mk3(va2.w, vb2.x, vb2.y);
+        f3 lp = add(add(muls(p0, bx), muls(p1, by)), muls(p2, bz));
+        f3 ln;
+        if (iszero3(n0) || iszero3(n1) || iszero3(n2)) ln = normalize(cross(sub(p1, p0), sub(p2, p0)));
+        else ln = add(add(muls(n0, bx), muls(n1, by)), muls(n2, bz));
+        ln = normalize(ln);
+        int lmat = __float_as_int(s.tris[3 * (size_t)triIndex + 2].y);
+        f3 ldir = sub(lp, P);
+        float dis2 = (ldir.x * ldir.x + ldir.y * ldir.y) + ldir.z * ldir.z;
+        f3 lightL = normalize(ldir);
+        pl = dis2 / (pnm_fabs(dot(ln, neg(lightL))) * s.lights_sum_area);
+        f3 li = get_emissive(s, lmat);
+        f3 lightBRDF = disney(bc, lightL);
+        LD = divs(muls(mul(lightBRDF, li), pnm_fabs(dot(N, lightL))), pl);
+        b.R0[i] = make_float4(ldir.x, ldir.y, ldir.z, 0.f);
+        nfl |= WF_RLIGHT;
+    }
+    // environment (:911-926)
+    f3 LE = mk3(0.f, 0.f, 0.f);
+    float pe = 0.f;
+    if (s.has_hdr) {
+        float r1 = rand01(seed), r2 = rand01(seed);
+        f3 enL;
+        f3 enLi = sample_env(s, r1, r2, enL, pe);
+        if (dot(enL, N) > 0) {
+            f3 dB = disney(bc, enL);
+            LE = divs(muls(mul(dB, enLi), dot(enL, N)), pe);
+            b.R1[i] = make_float4(enL.x, enL.y, enL.z, 0.f);
+            nfl |= WF_RENV;
+        }
+    }
+    // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
+    uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
+                      (uint32_t)(114514 / 1919) * 26699u) | 1u;
+    float cpu = rand01(pseed), cpv = rand01(pseed);
+    const uint32_t g = (frame + 1u) ^ ((frame + 1u) >> 1);
+    float su = sobol_dev(2u * (uint32_t)bounce, g), sv = sobol_dev(2u * (uint32_t)bounce + 1u, g);
+    su += cpu; if (su > 1) su -= 1; if (su < 0) su += 1;
+    sv += cpv; if (sv > 1) sv -= 1; if (sv < 0) sv += 1;
+    float rDiffuse = 1.0f - m.metallic;
+    float rClearcoat = 0.25f * m.clearcoat;
+    float invSum = 1.0f / ((rDiffuse + 1.0f) + rClearcoat);
+    float pDiffuse = rDiffuse * invSum, pSpecular = 1.0f * invSum, pClearcoat = rClearcoat * invSum;
+    float rl = rand01(seed);
+    float alphaGTR1 = bc.alphaDr;
+    float alphaGTR2 = fmax_(0.001f, sqr(m.roughness));
+    f3 L;
+    if (rl <= pDiffuse) {
+        float theta = rand01(seed), rr = rand01(seed);
+        float sth, cth;
+        pnm_sincos(theta, sth, cth);
+        float xx = rr * sth, yy = rr * cth;
+        float zz = sqrtf((1.0f - sqr(xx)) - sqr(yy));
+        L = tangent_to_world(T, B, N, mk3(xx, yy, zz));
+    } else {
+        float phiH = (2.0f * PT_PI) * su;
+        float cosThetaH;
+        if (rl <= pDiffuse + pSpecular)
+            cosThetaH = sqrtf((1.0f - sv) / (1.0f + ((alphaGTR2 * alphaGTR2) - 1.0f) * sv));
+        else {
+            float a2 = alphaGTR1 * alphaGTR1;
+            cosThetaH = sqrtf((1.0f - pnm_pow(a2, 1.0f - sv)) / (1.0f - a2));
+        }
+        float sinThetaH = fmax_(0.0f, 1.0f - sqr(cosThetaH));
+        float sinPhiH = pnm_sin(phiH), cosPhiH = 1.0f - sqr(sinPhiH);
+        f3 h = tangent_to_world(T, B, N, mk3(sinThetaH * cosPhiH, sinThetaH * sinPhiH, cosThetaH));
+        L = sub(smul(2.0f * dot(V, h), h), V);
+    }
+    f3 H = normalize(add(L, V));
+    float LdotH = dot(L, H), NdotH = dot(N, H), NdotLs = dot(N, L);
+    float pdfDiffuse = NdotLs * PT_INVPI;
+    float pdfSpecular = (gtr2(NdotH, alphaGTR2) * NdotH) / (4.0f * LdotH);
+    float pdfClearcoat = (gtr1(NdotH, alphaGTR1) * NdotH) / (4.0f * LdotH);
+    float dPDF = (pDiffuse * pdfDiffuse + pSpecular * pdfSpecular) + pClearcoat * pdfClearcoat;
+    f3 dBRDF = disney(bc, L);
+    float NdotL = pnm_fabs(dot(N, L));
+    b.C0[i] = make_float4(LD.x, LD.y, LD.z, pl);
+    b.C1[i] = make_float4(LE.x, LE.y, LE.z, pe);
+    b.C2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, NdotL);
+    b.C3[i] = make_float4(L.x, L.y, L.z, dPDF);
+    b.S3[i] = make_float4(s3.x, s3.y, s3.z, __uint_as_float(seed));
+    b.flags[i] = nfl | WF_RCONT;
+}
+
+// ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
+struct WfRay {
+    RayP r;
+    float tMax;
+    int hitTri;
+    uint32_t cur;
+    int lt, lc, sp;
+    uint32_t id;      // ray index
+    bool any, busy;
+};
+
+PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, float z) {
+    uint2 e = make_uint2(ref, __float_as_uint(z));
+    if (sp < WF_STACK) lds[sp * WF_TRACE_BLOCK + lane] = e;
+    else ovf[sp - WF_STACK] = e;
+    ++sp;
+}
+PN_DEV uint2 wf_pop(const uint2* lds, const uint2* ovf, int lane, int& sp) {
+    --sp;
+    return sp < WF_STACK ? lds[sp * WF_TRACE_BLOCK + lane] : ovf[sp - WF_STACK];
+}
+
+// BoundIntersect (:213-228) for traversal decisions.  fminf/fmaxf (v_min/v_max)
+// drop NaNs exactly like the oracle's min/max; the results only feed
+// comparisons, where the sign of a zero cannot matter -> same booleans.
+PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                     float& zlo) {
+    float fx = (mxx - r.o.x) * r.inv.x, fy = (mxy - r.o.y) * r.inv.y, fz = (mxz - r.o.z) * r.inv.z;
+    float nx = (mnx - r.o.x) * r.inv.x, ny = (mny - r.o.y) * r.inv.y, nz = (mnz - r.o.z) * r.inv.z;
+    float t1 = fminf(fmaxf(fx, nx), fminf(fmaxf(fy, ny), fmaxf(fz, nz)));
+    float t0 = fmaxf(fminf(fx, nx), fmaxf(fminf(fy, ny), fminf(fz, nz)));
+    float zf = r.kz == 2 ? fz : (r.kz == 0 ? fx : fy);
+    float zn = r.kz == 2 ? nz : (r.kz == 0 ? nx : ny);
+    float lo = zn < zf ? zn : zf, hi = zn < zf ? zf : zn;
+    zlo = lo;
+    // zhi <= 0: the whole box is behind the ray in the triangle test's frame
+    return (t1 >= t0) && !(r.cull_ok && hi <= 0.0f);
+}
+
+__global__ void __launch_bounds__(WF_TRACE_BLOCK) pt_wf_trace(DevScene s, WfBufs b, int mode) {
+    __shared__ uint2 lds[WF_STACK * WF_TRACE_BLOCK];
+    const int tl = threadIdx.x, lane = tl & 63;
+    const uint32_t n_rays = 3u * b.n;
+    const uint32_t n_waves = gridDim.x * (WF_TRACE_BLOCK / 64);
+    const uint32_t wave_id = blockIdx.x * (WF_TRACE_BLOCK / 64) + (tl >> 6);
+    // static contiguous range per wave: ray kinds are major, so a wave's rays share a kind
+    const uint32_t per = (n_rays + n_waves - 1) / n_waves;
+    uint32_t next = wave_id * per, end = min(next + per, n_rays);
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    uint2* ovf = b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * WF_OVF;
+    WfRay t;
+    t.busy = false;
+    t.sp = 0; t.lc = 0; t.cur = REF_NONE; t.hitTri = -1; t.tMax = 0.f; t.id = 0; t.any = true;
+    for (;;) {
+        // refill idle lanes with the wave's next rays (skipping rays that do not exist)
+        for (;;) {
+            uint64_t idle = __ballot(!t.busy);
+            if (idle == 0 || next >= end) break;
+            uint32_t myid = next + (uint32_t)__popcll(idle & lt_mask);
+            next = min(next + (uint32_t)__popcll(idle), end);
+            if (!t.busy && myid < end) {
+                uint32_t kind = myid / b.n, p = myid - kind * b.n;
+                uint32_t fl = b.flags[p];
+                uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
+                if ((fl & WF_ALIVE) && (fl & need)) {
+                    float4 s0 = b.S0[p], s1 = b.S1[p];
+                    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
+                    f3 o, d;
+                    float tmax;
+                    if (kind == 0) { float4 r = b.R0[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = 1.0f - PT_SHADOW_EPS; }
+                    else if (kind == 1) { float4 r = b.R1[p]; o = P; d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
+                    else { float4 r = b.C3[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
+                    t.r = make_ray(o, d, mode);
+                    t.tMax = tmax;
+                    t.hitTri = -1;
+                    t.any = kind != 2;
+                    t.id = myid;
+                    t.sp = 0; t.lc = 0;
+                    float zlo;
+                    if (box_fast(t.r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                                 s.root_max[2], zlo)) {
+                        t.cur = s.root_ref;
+                        if (t.cur & REF_LEAF) { decode_leaf(s, t.cur, t.lt, t.lc); t.cur = REF_NONE; }
+                    } else {
+                        t.cur = REF_NONE;
+                    }
+                    t.busy = true;
+                }
+            }
+        }
+        uint64_t busy = __ballot(t.busy);
+        if (busy == 0) break;
+        const int thr = __popcll(busy) / 2;
+        // traverse until half the lanes have finished their ray
+        for (;;) {
+            bool done = false;
+            if (t.busy) {
+                if (t.lc > 0) {
+                    const float4* tp = s.tris + 3 * (size_t)t.lt;
+                    float e0, e1, e2, det, ts;
+                    if (tri_test(t.r, tp[0], tp[1], tp[2], t.tMax, e0, e1, e2, det, ts)) {
+                        if (t.any) { done = true; t.hitTri = t.lt; }
+                        else { t.tMax = ts * (1.0f / det); t.hitTri = t.lt; }
+                    }
+                    ++t.lt; --t.lc;
+                } else if (t.cur == REF_NONE) {
+                    const float tmc = t.tMax * 1.000001f;
+                    for (;;) {
+                        if (t.sp == 0) { done = true; break; }
+                        uint2 e = wf_pop(lds, ovf, tl, t.sp);
+                        float z = __uint_as_float(e.y);
+                        if (t.r.cull_ok && z > tmc && z > 1e-20f) continue;
+                        if (e.x & REF_LEAF) decode_leaf(s, e.x, t.lt, t.lc);
+                        else t.cur = e.x;
+                        break;
+                    }
+                } else {
+                    const float4* nd = s.nodes + 4 * (size_t)t.cur;
+                    float4 a = nd[0], bb = nd[1], c = nd[2];
+                    uint4 m = *reinterpret_cast<const uint4*>(nd + 3);
+                    const float tmc = t.tMax * 1.000001f;
+                    float zloL, zloR;
+                    bool hL = box_fast(t.r, a.x, a.y, a.z, a.w, bb.x, bb.y, zloL);
+                    bool hR = box_fast(t.r, bb.z, bb.w, c.x, c.y, c.z, c.w, zloR);
+                    if (t.r.cull_ok) {
+                        if (zloL > tmc && zloL > 1e-20f) hL = false;
+                        if (zloR > tmc && zloR > 1e-20f) hR = false;
+                    }
+                    bool rightFirst = comp(t.r.d, (int)m.z) < 0;     // :448
+                    uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+                    bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+                    float zFar = rightFirst ? zloL : zloR;
+                    uint32_t go = REF_NONE;
+                    if (hNear) {
+                        if (hFar) wf_push(lds, ovf, tl, t.sp, farRef, zFar);
+                        go = nearRef;
+                    } else if (hFar) {
+                        go = farRef;
+                    }
+                    if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, t.lt, t.lc); go = REF_NONE; }
+                    t.cur = go;
+                }
+                if (done) {
+                    uint32_t kind = t.id / b.n, p = t.id - kind * b.n;
+                    if (kind == 2) b.hit[p] = t.hitTri;
+                    else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
+                    t.busy = false;
+                }
+            }
+            if (__popcll(__ballot(t.busy)) <= thr) break;
+        }
+    }
+}
+
+// ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
+__global__ void __launch_bounds__(256) pt_wf_shade(DevScene s, FrameParams fp, WfBufs b, float4* colors) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    uint32_t fl = b.flags[i];
+    if (!(fl & WF_ALIVE)) return;
+    int bounce = (int)((fl >> 8) & 7u);
+    float4 c0 = b.C0[i], c1 = b.C1[i], c2 = b.C2[i], c3 = b.C3[i];
+    float4 s2 = b.S2[i], s3 = b.S3[i];
+    f3 LD = mk3(c0.x, c0.y, c0.z), LE = mk3(c1.x, c1.y, c1.z);
+    float pl = c0.w, pe = c1.w;
+    if ((fl & WF_RLIGHT) && b.occ[2 * (size_t)i]) { LD = mk3(0.f, 0.f, 0.f); pl = 0.f; }     // :890
+    if (!(fl & WF_RENV) || b.occ[2 * (size_t)i + 1]) LE = mk3(0.f, 0.f, 0.f);                 // :922
+    f3 dBRDF = mk3(c2.x, c2.y, c2.z), L = mk3(c3.x, c3.y, c3.z);
+    float NdotL = c2.w, dPDF = c3.w;
+    f3 Lo = mk3(s2.x, s2.y, s2.z), cw = mk3(s3.x, s3.y, s3.z);
+    float invPDFSum = 1.0f / ((pe + pl) + dPDF);
+    f3 mis = add(muls(LE, pe), muls(LD, pl));
+    Lo = add(Lo, muls(mul(cw, mis), invPDFSum));
+    int ht = b.hit[i];
+    int x, lr, k;
+    wf_coords(b, i, x, lr, k);
+    if (ht < 0) {
+        if (s.has_hdr) {
+            f3 enLi = env_color(s, normalize(L));
+            Lo = add(Lo, divs(muls(mul(mul(cw, enLi), dBRDF), NdotL), dPDF));
+        }
+        float4 s5 = b.S5[i];
+        wf_write_color(fp, colors, k, lr, x, add(mk3(s5.x, s5.y, s5.z), Lo));
+        b.flags[i] = 0;
+        return;
+    }
+    float4 s0 = b.S0[i], s1 = b.S1[i];
+    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
+    RayP r = make_ray(add(P, muls(N, 0.0001f)), L, 0);
+    Hit h = make_hit(s, r, ht);
+    f3 em = get_emissive(s, h.mat);
+    Lo = add(Lo, divs(muls(mul(mul(cw, em), dBRDF), NdotL), dPDF));
+    cw = mul(cw, divs(muls(dBRDF, NdotL), dPDF));
+    ++bounce;
+    if (bounce >= fp.max_depth) {
+        float4 s5 = b.S5[i];
+        wf_write_color(fp, colors, k, lr, x, add(mk3(s5.x, s5.y, s5.z), Lo));
+        b.flags[i] = 0;
+        return;
+    }
+    f3 V = neg(L);
+    b.S0[i] = make_float4(h.P.x, h.P.y, h.P.z, h.u);
+    b.S1[i] = make_float4(h.N.x, h.N.y, h.N.z, h.v);
+    b.S2[i] = make_float4(Lo.x, Lo.y, Lo.z, __int_as_float((h.mat & 0x00ffffff) | ((h.tex + 1) << 24)));
+    b.S3[i] = make_float4(cw.x, cw.y, cw.z, s3.w);
+    b.S4[i] = make_float4(V.x, V.y, V.z, 0.f);
+    b.flags[i] = WF_ALIVE | ((uint32_t)bounce << 8);
+}
