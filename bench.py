@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=["C2", "C4", "C5"])
     ap.add_argument("--mode", default="zcull", choices=["exact", "zcull"])
-    ap.add_argument("--kernel", default="v3", choices=["v1", "v2", "v3"])
+    ap.add_argument("--kernel", default="v3", choices=["v1", "v3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-image", default="")
@@ -93,7 +93,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from pnraytracing_amd import scenes
-    from pnraytracing_amd.tracer import KERNEL_V1, KERNEL_V2, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, shard_rows
+    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, shard_rows
 
     builders = {"C2": scenes.bunny_c2, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
     cfg = builders[args.config]()
@@ -103,7 +103,7 @@ def main():
     stream = torch.cuda.Stream()               # a real stream handle (the default one is NULL)
     torch.cuda.set_stream(stream)
     pt.set_stream(stream.cuda_stream)
-    opts = (TRAVERSE_ZCULL if args.mode == "zcull" else TRAVERSE_EXACT) | {"v1": KERNEL_V1, "v2": KERNEL_V2, "v3": 0}[args.kernel]
+    opts = (TRAVERSE_ZCULL if args.mode == "zcull" else TRAVERSE_EXACT) | {"v1": KERNEL_V1, "v3": 0}[args.kernel]
     pt.load(cfg, opts)
     info = pt.device_info()
 
@@ -181,7 +181,7 @@ def main():
             "config": {"workload": f"{cfg.name}: {cfg.description}", "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
-                       "kernel": {"v1": "pt_render_kernel", "v2": "pt_wave_kernel", "v3": "pt_wf_trace"}[args.kernel]},
+                       "kernel": {"v1": "pt_render_kernel", "v3": "pt_wf_trace"}[args.kernel]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

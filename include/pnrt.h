@@ -49,7 +49,6 @@ typedef struct {
 #define PNRT_TRAVERSE_EXACT 0   /* the reference's box visits (no tMax culling)      */
 #define PNRT_TRAVERSE_ZCULL 1   /* + provably result-neutral z-slab culling (default) */
 #define PNRT_KERNEL_V1 0x100    /* A/B baseline: one lane per pixel, frames in-lane        */
-#define PNRT_KERNEL_V2 0x200    /* A/B baseline: persistent state-machine megakernel       */
                                 /* default: wavefront (setup / trace / shade per bounce)   */
 
 const char* pnrt_version(void);

@@ -25,7 +25,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PNRT_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SRCS = ["pnrt_device.hip"]
-DEVICE_DEPS = ["pnrt_device.hip", "pt_common.h", "pt_kernel.h", "pt_shade.h", "pn_math.h", "sobol_v.inc"]
+DEVICE_DEPS = ["pnrt_device.hip", "pt_common.h", "pt_kernel.h", "pt_shade.h", "pt_path.h", "pt_passes.h", "pt_wf.h",
+               "pn_math.h", "sobol_v.inc"]
 
 
 def _run(cmd, cwd=None):
@@ -53,7 +54,7 @@ def build_device(force=False, extra=()):
     out = os.path.join(PKG, "libpnrt.so")
     deps = [os.path.join(CSRC, d) for d in DEVICE_DEPS] + [os.path.join(INC, "pnrt.h")]
     if force or extra or _stale(out, deps):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+        cmd = [HIPCC, f"--offload-arch={ARCH}", os.environ.get("PNRT_OPT", "-O3"), "-std=c++17", "-fPIC", "-shared",
                "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-rdc", "-I", INC,
                *extra, *[os.path.join(CSRC, s) for s in DEVICE_SRCS], "-o", out]
         _run(cmd)

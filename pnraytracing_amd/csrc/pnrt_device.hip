@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -15,7 +16,6 @@
 #include "../../include/pnrt.h"
 
 #include "pt_path.h"
-#include "pt_wave.h"
 #include "pt_wf.h"
 
 __global__ void pt_pack_rows_kernel(const float4* accum, float4* dst, int width, int rows, int band,
@@ -76,17 +76,15 @@ struct pnrt_ctx {
     bool has_frame = false;
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
-    int kernel = 3;                        // 3 = wavefront (default), 2 = persistent megakernel, 1 = v1
-    // v2 work buffers (grown on demand)
+    int kernel = 3;                        // 3 = wavefront (default), 1 = v1 one-lane-per-pixel
+    // wavefront buffers (grown on demand)
     float4* primary = nullptr;  size_t primary_cap = 0;
     float4* colors = nullptr;   size_t colors_cap = 0;
-    uint2* ovf = nullptr;       size_t ovf_cap = 0;
-    unsigned int* counter = nullptr;
-    int wave_grid = 0;
-    // v3 wavefront buffers
     void* wf = nullptr;         size_t wf_cap = 0;
     uint2* wf_ovf = nullptr;    size_t wf_ovf_cap = 0;
     int trace_grid = 0;
+    bool debug_simple_trace = false;
+    int debug_variant = 0;
 };
 
 static int set_err(pnrt_ctx* c, int code, const std::string& m) {
@@ -100,7 +98,7 @@ static int set_err(pnrt_ctx* c, int code, const std::string& m) {
             return set_err(ctx, PNRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
     } while (0)
 
-#define PTW_MAX_CHUNK_FRAMES 8
+#define WF_MAX_CHUNK_FRAMES 8
 
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
@@ -138,12 +136,12 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 // x max_depth -> ordered blend.
 static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
     const size_t pix = (size_t)fp.rows * c->width;
-    const uint32_t chunk = nf < PTW_MAX_CHUNK_FRAMES ? nf : PTW_MAX_CHUNK_FRAMES;
+    const uint32_t chunk = nf < WF_MAX_CHUNK_FRAMES ? nf : WF_MAX_CHUNK_FRAMES;
     const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
     const size_t nmax = (size_t)tiles_x * tiles_y * 64 * chunk;
     if (c->trace_grid == 0) {
         int per_cu = 0, cus = 0;
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace, WF_TRACE_BLOCK, 0));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false>, WF_TRACE_BLOCK, 0));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
@@ -178,7 +176,41 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         HIPCHK(c, hipGetLastError());
         for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
             hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
-            hipLaunchKernelGGL(pt_wf_trace, dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            if (c->debug_simple_trace)
+                hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b,
+                                   fp.mode);
+            else if (c->debug_variant == 1)   // deep LDS stack, no spill
+                hipLaunchKernelGGL((pt_wf_trace<48, false>), dim3(256), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            else if (c->debug_variant == 2)   // refill only when every lane is idle
+                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            else
+                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            if (c->debug_variant == 9) {   // compare every ray with the simple kernel
+                std::vector<int> h1(n), h2(n);
+                std::vector<uint8_t> o1(2 * n), o2(2 * n);
+                std::vector<uint32_t> fl(n);
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                HIPCHK(c, hipMemcpy(h1.data(), b.hit, n * 4, hipMemcpyDeviceToHost));
+                HIPCHK(c, hipMemcpy(o1.data(), b.occ, 2 * n, hipMemcpyDeviceToHost));
+                HIPCHK(c, hipMemcpy(fl.data(), b.flags, n * 4, hipMemcpyDeviceToHost));
+                hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b, fp.mode);
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                HIPCHK(c, hipMemcpy(h2.data(), b.hit, n * 4, hipMemcpyDeviceToHost));
+                HIPCHK(c, hipMemcpy(o2.data(), b.occ, 2 * n, hipMemcpyDeviceToHost));
+                size_t bad[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
+                long first[3] = {-1, -1, -1};
+                for (size_t p = 0; p < n; ++p) {
+                    if (!(fl[p] & WF_ALIVE)) continue;
+                    if (fl[p] & WF_RLIGHT) { tot[0]++; if (o1[2 * p] != o2[2 * p]) { if (first[0] < 0) first[0] = (long)p; bad[0]++; } }
+                    if (fl[p] & WF_RENV) { tot[1]++; if (o1[2 * p + 1] != o2[2 * p + 1]) { if (first[1] < 0) first[1] = (long)p; bad[1]++; } }
+                    if (fl[p] & WF_RCONT) { tot[2]++; if (h1[p] != h2[p]) { if (first[2] < 0) first[2] = (long)p; bad[2]++; } }
+                }
+                fprintf(stderr, "[trace check] bounce %d: light %zu/%zu env %zu/%zu cont %zu/%zu mismatches; first p=%ld/%ld/%ld",
+                        bounce, bad[0], tot[0], bad[1], tot[1], bad[2], tot[2], first[0], first[1], first[2]);
+                if (first[0] >= 0) fprintf(stderr, " light p%ld persistent=%d simple=%d", first[0], o1[2 * first[0]], o2[2 * first[0]]);
+                if (first[2] >= 0) fprintf(stderr, " cont p%ld persistent=%d simple=%d", first[2], h1[first[2]], h2[first[2]]);
+                fprintf(stderr, "\n");
+            }
             hipLaunchKernelGGL(pt_wf_shade, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
             HIPCHK(c, hipGetLastError());
         }
@@ -205,6 +237,12 @@ int pnrt_create(int device, pnrt_ctx** out) {
         return PNRT_E_HIP;
     }
     c->stream = c->own_stream;
+    {
+        const char* e = getenv("PNRT_DEBUG_SIMPLE_TRACE");
+        c->debug_simple_trace = e && e[0] == '1';
+        const char* v = getenv("PNRT_DEBUG_TRACE_VARIANT");
+        c->debug_variant = v ? atoi(v) : 0;
+    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_sobolV), kSobolV, sizeof kSobolV) != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;
@@ -231,7 +269,7 @@ void pnrt_destroy(pnrt_ctx* c) {
     for (void* t : c->tex) (void)hipFree(t);
     (void)hipFree(c->unorm8);
     (void)hipFree(c->accum);
-    (void)hipFree(c->primary); (void)hipFree(c->colors); (void)hipFree(c->ovf); (void)hipFree(c->counter);
+    (void)hipFree(c->primary); (void)hipFree(c->colors);
     (void)hipFree(c->wf); (void)hipFree(c->wf_ovf);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -248,11 +286,10 @@ int pnrt_set_stream(pnrt_ctx* c, void* s) {
 int pnrt_set_options(pnrt_ctx* c, int options) {
     if (!c) return PNRT_E_ARG;
     int mode = options & 0xff;
-    if ((mode != PNRT_TRAVERSE_EXACT && mode != PNRT_TRAVERSE_ZCULL) || (options & ~0x3ff) ||
-        ((options & PNRT_KERNEL_V1) && (options & PNRT_KERNEL_V2)))
+    if ((mode != PNRT_TRAVERSE_EXACT && mode != PNRT_TRAVERSE_ZCULL) || (options & ~0x1ff))
         return set_err(c, PNRT_E_ARG, "unknown option bits");
     c->mode = mode;
-    c->kernel = (options & PNRT_KERNEL_V1) ? 1 : (options & PNRT_KERNEL_V2) ? 2 : 3;
+    c->kernel = (options & PNRT_KERNEL_V1) ? 1 : 3;
     return PNRT_OK;
 }
 
@@ -480,46 +517,8 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
         HIPCHK(c, hipGetLastError());
         return PNRT_OK;
     }
-    if (c->kernel == 3) return render_wavefront(c, s, fp, first, nf);
-    // ---- v2: primary pass, persistent megakernel per frame chunk, ordered blend
-    if (!c->counter) HIPCHK(c, hipMalloc(&c->counter, 64));
-    if (c->wave_grid == 0) {
-        int per_cu = 0, cus = 0;
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wave_kernel, PTW_BLOCK, 0));
-        HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        c->wave_grid = (per_cu > 0 ? per_cu : 1) * cus;
-    }
-    const size_t pix = (size_t)fp.rows * c->width;
-    const uint32_t chunk = nf < PTW_MAX_CHUNK_FRAMES ? nf : PTW_MAX_CHUNK_FRAMES;
-    int rc;
-    if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
-        (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, (void**)&c->ovf, &c->ovf_cap, (size_t)c->wave_grid * PTW_BLOCK * PTW_OVF_STACK * 8)))
-        return rc;
-    hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, s, fp,
-                       c->primary);
-    HIPCHK(c, hipGetLastError());
-    const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
-    for (uint32_t f0 = 0; f0 < nf; f0 += chunk) {
-        uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
-        WaveArgs wa;
-        wa.primary = c->primary;
-        wa.colors = c->colors;
-        wa.accum = c->accum;
-        wa.ovf = c->ovf;
-        wa.counter = c->counter;
-        wa.total_samples = (uint32_t)((size_t)tiles_x * tiles_y * 64 * cf);
-        wa.tiles_x = tiles_x;
-        wa.chunk_frames = (int)cf;
-        wa.first_frame = first + f0;
-        HIPCHK(c, hipMemsetAsync(c->counter, 0, 4, c->stream));
-        hipLaunchKernelGGL(pt_wave_kernel, dim3(c->wave_grid), dim3(PTW_BLOCK), 0, c->stream, s, fp, wa);
-        HIPCHK(c, hipGetLastError());
-        hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
-                           (const float4*)c->colors, c->accum, (int)cf, first + f0);
-        HIPCHK(c, hipGetLastError());
-    }
-    return PNRT_OK;
+    return render_wavefront(c, s, fp, first, nf);
+    return set_err(c, PNRT_E_STATE, "unknown kernel variant");
 }
 
 int pnrt_reset_accum(pnrt_ctx* c) {

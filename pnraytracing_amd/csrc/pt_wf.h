@@ -12,7 +12,7 @@
 //             hit (emission, throughput), next bounce or the final colour
 // so each kernel is compact and coherent instead of one 240-VGPR megakernel.
 #pragma once
-#include "pt_wave.h"
+#include "pt_passes.h"
 
 #define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
 #define WF_OVF 56
@@ -51,7 +51,8 @@ struct WfBufs {
     uint32_t first_frame;
 };
 
-// path slot -> (x, local row, frame slot): same tile order as the v2 kernel
+// path slot -> (x, local row, frame slot): 8x8-pixel tiles, frame-major inside a
+// tile, so consecutive path slots (and the rays they spawn) are spatial neighbours
 PN_DEV void wf_coords(const WfBufs& b, uint32_t s, int& x, int& lr, int& k) {
     uint32_t per_tile = 64u * (uint32_t)b.chunk_frames;
     uint32_t tile = s / per_tile, rem = s - tile * per_tile;
@@ -217,25 +218,17 @@ __global__ void __launch_bounds__(256) pt_wf_setup(DevScene s, FrameParams fp, W
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
-struct WfRay {
-    RayP r;
-    float tMax;
-    int hitTri;
-    uint32_t cur;
-    int lt, lc, sp;
-    uint32_t id;      // ray index
-    bool any, busy;
-};
-
+template <int STK>
 PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, float z) {
     uint2 e = make_uint2(ref, __float_as_uint(z));
-    if (sp < WF_STACK) lds[sp * WF_TRACE_BLOCK + lane] = e;
-    else ovf[sp - WF_STACK] = e;
+    if (sp < STK) lds[sp * WF_TRACE_BLOCK + lane] = e;
+    else ovf[sp - STK] = e;
     ++sp;
 }
+template <int STK>
 PN_DEV uint2 wf_pop(const uint2* lds, const uint2* ovf, int lane, int& sp) {
     --sp;
-    return sp < WF_STACK ? lds[sp * WF_TRACE_BLOCK + lane] : ovf[sp - WF_STACK];
+    return sp < STK ? lds[sp * WF_TRACE_BLOCK + lane] : ovf[sp - STK];
 }
 
 // BoundIntersect (:213-228) for traversal decisions.  fminf/fmaxf (v_min/v_max)
@@ -255,117 +248,132 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return (t1 >= t0) && !(r.cull_ok && hi <= 0.0f);
 }
 
+// Fetch ray `id` of the bounce into a lane (false if that ray does not exist).
+PN_DEV bool wf_load_ray(const DevScene& s, const WfBufs& b, uint32_t id, int mode, RayP& r, float& tmax, bool& any) {
+    uint32_t kind = id / b.n, p = id - kind * b.n;
+    uint32_t fl = b.flags[p];
+    uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
+    if (!((fl & WF_ALIVE) && (fl & need))) return false;
+    float4 s0 = b.S0[p], s1 = b.S1[p];
+    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
+    float4 dv = kind == 0 ? b.R0[p] : (kind == 1 ? b.R1[p] : b.C3[p]);
+    f3 o = kind == 1 ? P : add(P, muls(N, 0.0001f));
+    tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
+    any = kind != 2;
+    r = make_ray(o, mk3(dv.x, dv.y, dv.z), mode);
+    return true;
+}
+
+// Persistent traversal of every ray of the bounce.  Control flow is kept
+// structured and loop-free inside a lane's step (one triangle test, one node,
+// or one stack pop per iteration) with every wave-level decision (ballot) at a
+// reconvergence point: the ray <-> lane refill runs once per outer iteration.
+template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK) pt_wf_trace(DevScene s, WfBufs b, int mode) {
-    __shared__ uint2 lds[WF_STACK * WF_TRACE_BLOCK];
+    __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
     const int tl = threadIdx.x, lane = tl & 63;
     const uint32_t n_rays = 3u * b.n;
     const uint32_t n_waves = gridDim.x * (WF_TRACE_BLOCK / 64);
     const uint32_t wave_id = blockIdx.x * (WF_TRACE_BLOCK / 64) + (tl >> 6);
-    // static contiguous range per wave: ray kinds are major, so a wave's rays share a kind
+    // static contiguous range per wave (ray kinds are major, so a wave's rays share a kind)
     const uint32_t per = (n_rays + n_waves - 1) / n_waves;
-    uint32_t next = wave_id * per, end = min(next + per, n_rays);
+    uint32_t next = min(wave_id * per, n_rays);
+    const uint32_t end = min(next + per, n_rays);
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint2* ovf = b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * WF_OVF;
-    WfRay t;
-    t.busy = false;
-    t.sp = 0; t.lc = 0; t.cur = REF_NONE; t.hitTri = -1; t.tMax = 0.f; t.id = 0; t.any = true;
+
+    RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
+    float tMax = 0.f;
+    int hitTri = -1, lt = 0, lc = 0, sp = 0;
+    uint32_t cur = REF_NONE, rid = 0;
+    bool any = true;
+    int busy = 0;
+
     for (;;) {
-        // refill idle lanes with the wave's next rays (skipping rays that do not exist)
-        for (;;) {
-            uint64_t idle = __ballot(!t.busy);
-            if (idle == 0 || next >= end) break;
-            uint32_t myid = next + (uint32_t)__popcll(idle & lt_mask);
+        // ---- refill (one pass): idle lanes take the wave's next ray ids -------------------
+        const uint64_t idle = __ballot(busy == 0);
+        if (idle != 0 && next < end) {
+            const uint32_t myid = next + (uint32_t)__popcll(idle & lt_mask);
             next = min(next + (uint32_t)__popcll(idle), end);
-            if (!t.busy && myid < end) {
-                uint32_t kind = myid / b.n, p = myid - kind * b.n;
-                uint32_t fl = b.flags[p];
-                uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
-                if ((fl & WF_ALIVE) && (fl & need)) {
-                    float4 s0 = b.S0[p], s1 = b.S1[p];
-                    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
-                    f3 o, d;
-                    float tmax;
-                    if (kind == 0) { float4 r = b.R0[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = 1.0f - PT_SHADOW_EPS; }
-                    else if (kind == 1) { float4 r = b.R1[p]; o = P; d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
-                    else { float4 r = b.C3[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
-                    t.r = make_ray(o, d, mode);
-                    t.tMax = tmax;
-                    t.hitTri = -1;
-                    t.any = kind != 2;
-                    t.id = myid;
-                    t.sp = 0; t.lc = 0;
+            if (busy == 0 && myid < end) {
+                RayP nr;
+                float ntmax;
+                bool nany;
+                if (wf_load_ray(s, b, myid, mode, nr, ntmax, nany)) {
                     float zlo;
-                    if (box_fast(t.r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                    uint32_t root = REF_NONE;
+                    int nlt = 0, nlc = 0;
+                    if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
                                  s.root_max[2], zlo)) {
-                        t.cur = s.root_ref;
-                        if (t.cur & REF_LEAF) { decode_leaf(s, t.cur, t.lt, t.lc); t.cur = REF_NONE; }
-                    } else {
-                        t.cur = REF_NONE;
+                        root = s.root_ref;
+                        if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
-                    t.busy = true;
+                    r = nr; tMax = ntmax; any = nany; rid = myid;
+                    hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
+                    busy = 1;
                 }
             }
         }
-        uint64_t busy = __ballot(t.busy);
-        if (busy == 0) break;
-        const int thr = __popcll(busy) / 2;
-        // traverse until half the lanes have finished their ray
+        const uint64_t busym = __ballot(busy != 0);
+        if (busym == 0) {
+            if (next >= end) break;
+            continue;
+        }
+        const int thr = SYNC ? 0 : __popcll(busym) / 2;
+        // ---- traverse until half of the lanes have finished their ray ------------------
         for (;;) {
-            bool done = false;
-            if (t.busy) {
-                if (t.lc > 0) {
-                    const float4* tp = s.tris + 3 * (size_t)t.lt;
+            if (busy) {
+                bool done = false;
+                if (lc > 0) {
+                    const float4* tp = s.tris + 3 * (size_t)lt;
                     float e0, e1, e2, det, ts;
-                    if (tri_test(t.r, tp[0], tp[1], tp[2], t.tMax, e0, e1, e2, det, ts)) {
-                        if (t.any) { done = true; t.hitTri = t.lt; }
-                        else { t.tMax = ts * (1.0f / det); t.hitTri = t.lt; }
+                    if (tri_test(r, tp[0], tp[1], tp[2], tMax, e0, e1, e2, det, ts)) {
+                        hitTri = lt;
+                        if (any) done = true;
+                        else tMax = ts * (1.0f / det);
                     }
-                    ++t.lt; --t.lc;
-                } else if (t.cur == REF_NONE) {
-                    const float tmc = t.tMax * 1.000001f;
-                    for (;;) {
-                        if (t.sp == 0) { done = true; break; }
-                        uint2 e = wf_pop(lds, ovf, tl, t.sp);
+                    ++lt; --lc;
+                } else if (cur == REF_NONE) {
+                    if (sp == 0) {
+                        done = true;
+                    } else {
+                        uint2 e = wf_pop<STK>(lds, ovf, tl, sp);
                         float z = __uint_as_float(e.y);
-                        if (t.r.cull_ok && z > tmc && z > 1e-20f) continue;
-                        if (e.x & REF_LEAF) decode_leaf(s, e.x, t.lt, t.lc);
-                        else t.cur = e.x;
-                        break;
+                        bool culled = r.cull_ok && z > tMax * 1.000001f && z > 1e-20f;
+                        if (!culled) {
+                            if (e.x & REF_LEAF) decode_leaf(s, e.x, lt, lc);
+                            else cur = e.x;
+                        }
                     }
                 } else {
-                    const float4* nd = s.nodes + 4 * (size_t)t.cur;
+                    const float4* nd = s.nodes + 4 * (size_t)cur;
                     float4 a = nd[0], bb = nd[1], c = nd[2];
                     uint4 m = *reinterpret_cast<const uint4*>(nd + 3);
-                    const float tmc = t.tMax * 1.000001f;
+                    const float tmc = tMax * 1.000001f;
                     float zloL, zloR;
-                    bool hL = box_fast(t.r, a.x, a.y, a.z, a.w, bb.x, bb.y, zloL);
-                    bool hR = box_fast(t.r, bb.z, bb.w, c.x, c.y, c.z, c.w, zloR);
-                    if (t.r.cull_ok) {
+                    bool hL = box_fast(r, a.x, a.y, a.z, a.w, bb.x, bb.y, zloL);
+                    bool hR = box_fast(r, bb.z, bb.w, c.x, c.y, c.z, c.w, zloR);
+                    if (r.cull_ok) {
                         if (zloL > tmc && zloL > 1e-20f) hL = false;
                         if (zloR > tmc && zloR > 1e-20f) hR = false;
                     }
-                    bool rightFirst = comp(t.r.d, (int)m.z) < 0;     // :448
+                    bool rightFirst = comp(r.d, (int)m.z) < 0;     // :448
                     uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
                     bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
                     float zFar = rightFirst ? zloL : zloR;
-                    uint32_t go = REF_NONE;
-                    if (hNear) {
-                        if (hFar) wf_push(lds, ovf, tl, t.sp, farRef, zFar);
-                        go = nearRef;
-                    } else if (hFar) {
-                        go = farRef;
-                    }
-                    if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, t.lt, t.lc); go = REF_NONE; }
-                    t.cur = go;
+                    if (hNear && hFar) wf_push<STK>(lds, ovf, tl, sp, farRef, zFar);
+                    uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
+                    if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
+                    cur = go;
                 }
                 if (done) {
-                    uint32_t kind = t.id / b.n, p = t.id - kind * b.n;
-                    if (kind == 2) b.hit[p] = t.hitTri;
-                    else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
-                    t.busy = false;
+                    uint32_t kind = rid / b.n, p = rid - kind * b.n;
+                    if (kind == 2) b.hit[p] = hitTri;
+                    else b.occ[2 * (size_t)p + kind] = hitTri >= 0 ? 1 : 0;
+                    busy = 0;
                 }
             }
-            if (__popcll(__ballot(t.busy)) <= thr) break;
+            if (__popcll(__ballot(busy != 0)) <= thr) break;
         }
     }
 }
@@ -423,4 +431,30 @@ __global__ void __launch_bounds__(256) pt_wf_shade(DevScene s, FrameParams fp, W
     b.S3[i] = make_float4(cw.x, cw.y, cw.z, s3.w);
     b.S4[i] = make_float4(V.x, V.y, V.z, 0.f);
     b.flags[i] = WF_ALIVE | ((uint32_t)bounce << 8);
+}
+
+// Debug/reference variant of pt_wf_trace: one thread per ray, the verified
+// traverse<> of the primary pass (selected with PNRT_DEBUG_SIMPLE_TRACE=1).
+__global__ void __launch_bounds__(256) pt_wf_trace_simple(DevScene s, WfBufs b, int mode) {
+    uint32_t myid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (myid >= 3u * b.n) return;
+    uint32_t kind = myid / b.n, p = myid - kind * b.n;
+    uint32_t fl = b.flags[p];
+    uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
+    if (!((fl & WF_ALIVE) && (fl & need))) return;
+    float4 s0 = b.S0[p], s1 = b.S1[p];
+    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
+    f3 o, d;
+    float tmax;
+    if (kind == 0) { float4 r = b.R0[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = 1.0f - PT_SHADOW_EPS; }
+    else if (kind == 1) { float4 r = b.R1[p]; o = P; d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
+    else { float4 r = b.C3[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
+    RayP r = make_ray(o, d, mode);
+    int hitTri = -1;
+    if (kind == 2) {
+        traverse<false>(s, r, tmax, hitTri);
+        b.hit[p] = hitTri;
+    } else {
+        b.occ[2 * (size_t)p + kind] = traverse<true>(s, r, tmax, hitTri) ? 1 : 0;
+    }
 }

@@ -17,7 +17,6 @@ from .host import PackedScene
 TRAVERSE_EXACT = 0
 TRAVERSE_ZCULL = 1
 KERNEL_V1 = 0x100      # | with a traverse mode: one-lane-per-pixel A/B baseline kernel
-KERNEL_V2 = 0x200      # | with a traverse mode: persistent state-machine megakernel (A/B baseline)
 
 
 class PnrtError(RuntimeError):

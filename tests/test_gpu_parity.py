@@ -11,7 +11,7 @@ import pytest
 
 import pyoracle
 from pnraytracing_amd import scenes as S
-from pnraytracing_amd.tracer import KERNEL_V1, KERNEL_V2, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, PnrtError
+from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, PnrtError
 
 pytestmark = pytest.mark.gpu
 
@@ -82,8 +82,7 @@ def test_math_bitwise(pt, fn):
 
 
 # ---- whole images ---------------------------------------------------------------------------
-@pytest.mark.parametrize("mode", [TRAVERSE_EXACT, TRAVERSE_ZCULL, TRAVERSE_ZCULL | KERNEL_V1,
-                                  TRAVERSE_ZCULL | KERNEL_V2])
+@pytest.mark.parametrize("mode", [TRAVERSE_EXACT, TRAVERSE_ZCULL, TRAVERSE_ZCULL | KERNEL_V1])
 @pytest.mark.parametrize("first,n", [(0, 1), (0, 4), (7, 3), (0, 11)])
 def test_c1_bitwise(pt, mode, first, n):
     c = cfg("C1")
@@ -102,7 +101,7 @@ def test_c1_depth_variants(pt):
         assert_bitwise(got, ref, f"C1 depth {depth}")
 
 
-@pytest.mark.parametrize("mode", [TRAVERSE_ZCULL, TRAVERSE_ZCULL | KERNEL_V1, TRAVERSE_ZCULL | KERNEL_V2])
+@pytest.mark.parametrize("mode", [TRAVERSE_ZCULL, TRAVERSE_ZCULL | KERNEL_V1])
 def test_c2_small_bitwise(pt, mode):
     c = cfg("C2", width=192, height=108, spp=4)
     got = gpu_render(pt, c, 0, 4, mode)
@@ -140,9 +139,8 @@ def test_traversal_modes_agree_fullsize(pt):
     a = gpu_render(pt, c, 0, 4, TRAVERSE_EXACT)
     b = gpu_render(pt, c, 0, 4, TRAVERSE_ZCULL)
     assert_bitwise(b, a, "exact vs zcull")
-    for kv in (KERNEL_V1, KERNEL_V2):
-        other = gpu_render(pt, c, 0, 4, TRAVERSE_ZCULL | kv)
-        assert_bitwise(other, a, f"kernel variant {kv:#x} vs default")
+    other = gpu_render(pt, c, 0, 4, TRAVERSE_ZCULL | KERNEL_V1)
+    assert_bitwise(other, a, "v1 kernel vs wavefront")
 
 
 def test_progressive_split_calls(pt):
