@@ -149,7 +149,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 1024)) ||
+        (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 4096)) ||
         (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * WF_OVF * 8)))
         return rc;
     hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, s, fp,
@@ -166,6 +166,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
         b.hit = reinterpret_cast<int*>(base + off); off += n * 4;
         b.occ = reinterpret_cast<uint8_t*>(base + off); off += n * 2;
+        off = (off + 255) & ~(size_t)255;
+        b.counter = reinterpret_cast<unsigned int*>(base + off); off += 256;
         b.ovf = c->wf_ovf;
         b.n = (uint32_t)n;
         b.chunk_frames = (int)cf;
@@ -176,6 +178,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         HIPCHK(c, hipGetLastError());
         for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
             hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
+            HIPCHK(c, hipMemsetAsync(b.counter, 0, 4, c->stream));
             if (c->debug_simple_trace)
                 hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b,
                                    fp.mode);

@@ -17,6 +17,7 @@
 #define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
 #define WF_OVF 56
 #define WF_TRACE_BLOCK 256
+#define WF_CHUNK 256u        // rays per dequeue
 
 // flags[path]: bit0 alive, bit1 light ray, bit2 env ray, bit3 continuation ray,
 // bits 8..10 bounce
@@ -45,6 +46,7 @@ struct WfBufs {
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
     uint2* ovf;        // traversal stack spill
+    unsigned int* counter;   // ray dequeue counter (zeroed before each trace launch)
     uint32_t n;        // path slots
     int chunk_frames;
     int tiles_x;
@@ -273,12 +275,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK) pt_wf_trace(DevScene s, WfBufs
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
     const int tl = threadIdx.x, lane = tl & 63;
     const uint32_t n_rays = 3u * b.n;
-    const uint32_t n_waves = gridDim.x * (WF_TRACE_BLOCK / 64);
-    const uint32_t wave_id = blockIdx.x * (WF_TRACE_BLOCK / 64) + (tl >> 6);
-    // static contiguous range per wave (ray kinds are major, so a wave's rays share a kind)
-    const uint32_t per = (n_rays + n_waves - 1) / n_waves;
-    uint32_t next = min(wave_id * per, n_rays);
-    const uint32_t end = min(next + per, n_rays);
+    // rays are dequeued in chunks of WF_CHUNK consecutive ids (kind-major order, so
+    // a chunk's rays share a kind and neighbouring pixels); one atomic per chunk
+    uint32_t next = 0, end = 0;
+    bool exhausted = false;
     const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     uint2* ovf = b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * WF_OVF;
 
@@ -292,6 +292,13 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK) pt_wf_trace(DevScene s, WfBufs
     for (;;) {
         // ---- refill (one pass): idle lanes take the wave's next ray ids -------------------
         const uint64_t idle = __ballot(busy == 0);
+        if (idle != 0 && next >= end && !exhausted) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(b.counter, WF_CHUNK);
+            base = __shfl(base, 0);
+            if (base >= n_rays) exhausted = true;
+            else { next = base; end = min(base + WF_CHUNK, n_rays); }
+        }
         if (idle != 0 && next < end) {
             const uint32_t myid = next + (uint32_t)__popcll(idle & lt_mask);
             next = min(next + (uint32_t)__popcll(idle), end);
@@ -316,7 +323,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK) pt_wf_trace(DevScene s, WfBufs
         }
         const uint64_t busym = __ballot(busy != 0);
         if (busym == 0) {
-            if (next >= end) break;
+            if (exhausted) break;
             continue;
         }
         const int thr = SYNC ? 0 : __popcll(busym) / 2;

@@ -15,11 +15,6 @@ while IFS= read -r grp; do
     rc=$?; echo "pass $i [$grp] $v rc=$rc"
     [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
   done
-done <<'GROUPS'
-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
-SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS
-FETCH_SIZE
-WRITE_SIZE
-TCC_HIT_sum TCC_MISS_sum
-TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE
+done <<GROUPS
+${PMC_GROUPS}
 GROUPS
