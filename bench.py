@@ -71,11 +71,19 @@ def cpu_baseline(cfg, target_s: float):
             break
     dt = time.perf_counter() - t
     n = tot["samples"]
-    bps = pyoracle.algorithmic_bytes(tot) / n
+    bps = {"bytes_per_sample": pyoracle.algorithmic_bytes(tot) / n,
+           "trace_bytes_per_sample": pyoracle.bounce_traversal_bytes(tot) / n}
     return ({"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
              "sample": f"{cfg.name}: {it} full {cfg.width}x{H} iterations x {cfg.spp} spp = {n} samples "
                        f"in {dt:.1f}s, oracle/pn_oracle.c OpenMP {threads} threads"},
             bps, tot)
+
+
+def stored(path, cfg_name):
+    path = os.path.join(REPO, "profiles", path)
+    if not os.path.exists(path):
+        return None
+    return json.load(open(path)).get(cfg_name)
 
 
 def main():
@@ -93,7 +101,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from pnraytracing_amd import scenes
-    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer, shard_rows
+    from pnraytracing_amd.dist import ShardedFrame
+    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer
 
     builders = {"C2": scenes.bunny_c2, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
     cfg = builders[args.config]()
@@ -107,25 +116,14 @@ def main():
     pt.load(cfg, opts)
     info = pt.device_info()
 
-    rows = [torch.as_tensor(shard_rows(H, BAND, world, r), device="cuda") for r in range(world)]
-    maxrows = max(len(r) for r in rows)
-    if world > 1:
-        sendbuf = torch.zeros((maxrows, W, 4), dtype=torch.float32, device="cuda")
-        recv = [torch.zeros_like(sendbuf) for _ in range(world)] if rank == 0 else None
-        image = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+    sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
+    image = None
 
-    def step(k, ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        pt.render(spp * k, spp, BAND, world, rank)
-        if ev is not None:
-            ev[1].record(stream)
+    def step(k):
+        nonlocal image
+        sf.render(spp * k, spp)
         if world > 1:
-            pt.pack_rows(sendbuf.data_ptr(), BAND, world, rank)
-            dist.gather(sendbuf, recv, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    image.index_copy_(0, rows[r], recv[r][: len(rows[r])])
+            image = sf.gather()                # one RCCL gather of the row bands to rank 0
 
     for k in range(args.warmup):
         step(k)
@@ -133,16 +131,22 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # live per-kernel timing: the library brackets every launch with HIP events
+    # recorded on the stream it launches on (pnrt_profile_enable)
+    pt.profile_enable(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, events[k])
+        step(args.warmup + k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    prof = pt.profile_read()
+    pt.profile_enable(False)
+    kname = {"v1": "v1", "v3": "trace"}[args.kernel]
+    k_ms_total, k_launches = prof[kname]
+    kern_ms = k_ms_total / max(k_launches, 1)                  # average launch duration
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -161,17 +165,26 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu, bps, _ = cpu_baseline(cfg, args.cpu_seconds)
         if bps is None:
-            bps = float(json.load(open(os.path.join(REPO, "profiles", "algorithmic_bytes.json")))[cfg.name]) \
-                if os.path.exists(os.path.join(REPO, "profiles", "algorithmic_bytes.json")) else None
-        rows0 = len(rows[0])
-        samples_per_launch = rows0 * W * spp
-        achieved = (bps * samples_per_launch / (kern_ms * 1e-3) / 1e9) if bps else None
+            bps = stored("algorithmic_bytes.json", cfg.name)
+        rows0 = sf.my_rows
+        samples_per_step = rows0 * W * spp
+        launches_per_step = k_launches / args.steps
+        achieved = path = None
+        if bps:
+            # dominant kernel: algorithmic bytes of one launch / its average duration
+            per_sample = bps["trace_bytes_per_sample"] if args.kernel == "v3" else bps["bytes_per_sample"]
+            bytes_per_launch = per_sample * samples_per_step / launches_per_step
+            achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+            # SURVEY 8d whole-path figure: all algorithmic bytes / wall time per step
+            path_gbs = bps["bytes_per_sample"] * samples_per_step * args.steps / elapsed / 1e9
+            path = {"bytes_per_sample": round(bps["bytes_per_sample"], 1), "achieved": round(path_gbs, 2),
+                    "frac": round(path_gbs / HBM_PEAK_GBS, 4)}
         traffic = None
-        pmc = os.path.join(REPO, "profiles", f"pmc_{cfg.name}.json")
-        if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch_full_frame")
-            if traffic is not None:
-                traffic = traffic * rows0 / H
+        pmc = stored("pmc.json", f"{cfg.name}/{kname}")
+        if pmc and pmc.get("hbm_bytes_per_launch"):
+            traffic = round(pmc["hbm_bytes_per_launch"] * rows0 / pmc.get("rows", H))
+        kernels = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / args.steps}
+                   for k, (ms, n) in prof.items() if n}
         line = {
             "metric": "Msamples/sec (whole node) at 1920x1080, 4spp/iter; fraction of HBM roofline",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -186,8 +199,11 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic,
-                         "bytes_per_sample": round(bps, 1) if bps else None,
-                         "kernel_ms": round(kern_ms, 4)},
+                         "kernel": {"v1": "pt_render_kernel", "v3": "pt_wf_trace"}[args.kernel],
+                         "kernel_ms": round(kern_ms, 4),
+                         "algorithmic_bytes_per_launch": round(bytes_per_launch) if bps else None,
+                         "path": path},
+            "kernels": kernels,
             "cpu_baseline": cpu,
             "device": {"bvh_interior_nodes": info["n_interior"], "max_depth": info["max_depth"],
                        "scene_bytes": info["device_bytes"]},

@@ -115,6 +115,25 @@ int pnrt_pack_rows(pnrt_ctx* ctx, void* dst_device, int band_rows, int n_shards,
 int pnrt_synchronize(pnrt_ctx* ctx);
 int pnrt_get_device_info(pnrt_ctx* ctx, pnrt_device_info* info);
 
+/* Per-kernel timing (not in the reference, which has no GPU timers): while
+ * enabled, every launch of a kernel class is bracketed by HIP events recorded on
+ * the launch stream; pnrt_profile_read synchronises and returns the summed
+ * event durations (ms) and launch counts.  Enabling (or disabling) resets. */
+#define PNRT_K_PRIMARY 0   /* primary hits, one trace per pixel per render call */
+#define PNRT_K_GEN 1       /* path state for the call's frames                  */
+#define PNRT_K_SETUP 2     /* per bounce: sampling + speculative BSDF, shadow rays */
+#define PNRT_K_TRACE 3     /* per bounce: persistent BVH traversal of all rays  */
+#define PNRT_K_SHADE 4     /* per bounce: MIS + continuation                    */
+#define PNRT_K_BLEND 5     /* progressive mean into the accumulation image      */
+#define PNRT_K_V1 6        /* PNRT_KERNEL_V1 single-kernel path                 */
+#define PNRT_K_COUNT 7
+typedef struct {
+    double ms[PNRT_K_COUNT];
+    int64_t launches[PNRT_K_COUNT];
+} pnrt_profile;
+int pnrt_profile_enable(pnrt_ctx* ctx, int on);
+int pnrt_profile_read(pnrt_ctx* ctx, pnrt_profile* out);
+
 /* Test hook: evaluate one PN-libm / IEEE primitive on the device (same fn
  * codes as the oracle's pno_math_eval); host in/out arrays of n floats. */
 int pnrt_debug_math(pnrt_ctx* ctx, int fn, const float* a, const float* b, float* out, int n);

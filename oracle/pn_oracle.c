@@ -745,7 +745,13 @@ static void shade_pixel(Ctx* c, float* px4) {
     Interaction isect;
     memset(&isect, 0, sizeof isect);
     v3 color;
-    if (!BVHIntersect(c, &ray, &isect)) {
+    const uint64_t np0 = c->st->node_pops, ns0 = c->st->sibling_tests, nt0 = c->st->tri_tests, nh0 = c->st->tri_hits;
+    const int prim_hit = BVHIntersect(c, &ray, &isect);
+    c->st->prim_node_pops += c->st->node_pops - np0;
+    c->st->prim_sibling_tests += c->st->sibling_tests - ns0;
+    c->st->prim_tri_tests += c->st->tri_tests - nt0;
+    c->st->prim_tri_hits += c->st->tri_hits - nh0;
+    if (!prim_hit) {
         color = GetHDRImageColor(c, ray.dir);
     } else {
         v3 em = GetMaterial(c, isect.materialId).emssive;
@@ -767,6 +773,8 @@ static void stats_add(pno_stats* d, const pno_stats* s) {
     d->env_samples += s->env_samples; d->env_lookups += s->env_lookups;
     d->albedo_bytes += s->albedo_bytes; d->accum_rmw += s->accum_rmw; d->traversals += s->traversals;
     if (s->stack_overflow) d->stack_overflow = 1;
+    d->prim_node_pops += s->prim_node_pops; d->prim_sibling_tests += s->prim_sibling_tests;
+    d->prim_tri_tests += s->prim_tri_tests; d->prim_tri_hits += s->prim_tri_hits;
 }
 
 int pno_render(const pno_scene* scene, const pno_frame* frame,

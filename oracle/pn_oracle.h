@@ -58,6 +58,10 @@ typedef struct {
     uint64_t env_lookups, albedo_bytes, accum_rmw;
     uint64_t traversals;
     int stack_overflow;          /* set if any traversal needed > 128 entries */
+    /* the camera-ray share of node_pops / sibling_tests / tri_tests / tri_hits
+     * (the GPU traces the un-jittered camera ray once per pixel per call, the
+     * bounce rays in its per-bounce traversal kernel) */
+    uint64_t prim_node_pops, prim_sibling_tests, prim_tri_tests, prim_tri_hits;
 } pno_stats;
 
 /* Render frames [first_frame, first_frame + n_frames) for the rows

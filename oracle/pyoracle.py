@@ -42,13 +42,15 @@ class Frame(ctypes.Structure):
 STAT_FIELDS = ["samples", "node_pops", "sibling_tests", "tri_tests", "tri_hits", "material_fetches",
                "light_probes", "light_samples", "env_samples", "env_lookups", "albedo_bytes", "accum_rmw",
                "traversals"]
+PRIM_FIELDS = ["prim_node_pops", "prim_sibling_tests", "prim_tri_tests", "prim_tri_hits"]
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [(f, ctypes.c_uint64) for f in STAT_FIELDS] + [("stack_overflow", ctypes.c_int)]
+    _fields_ = [(f, ctypes.c_uint64) for f in STAT_FIELDS] + [("stack_overflow", ctypes.c_int)] + \
+               [(f, ctypes.c_uint64) for f in PRIM_FIELDS]
 
     def as_dict(self):
-        d = {f: int(getattr(self, f)) for f in STAT_FIELDS}
+        d = {f: int(getattr(self, f)) for f in STAT_FIELDS + PRIM_FIELDS}
         d["stack_overflow"] = int(self.stack_overflow)
         return d
 
@@ -60,6 +62,18 @@ BYTES = {"node_pops": 48, "sibling_tests": 24, "tri_tests": 60, "tri_hits": 60, 
 
 def algorithmic_bytes(stats: dict) -> int:
     return sum(stats[k] * v for k, v in BYTES.items()) + stats["albedo_bytes"]
+
+
+TRAVERSAL = ("node_pops", "sibling_tests", "tri_tests")
+
+
+def bounce_traversal_bytes(stats: dict) -> int:
+    """Algorithmic bytes of the bounce rays' traversals (every BVHIntersect /
+    BVHIntersectP except the camera ray's): node pops, sibling pre-tests and
+    triangle tests of the SURVEY 8d table.  This is the work of the GPU's
+    per-bounce traversal kernel; the closest hit's attribute fetch (+60 B)
+    happens in its shade/setup kernels and is not included."""
+    return sum((stats[k] - stats["prim_" + k]) * BYTES[k] for k in TRAVERSAL)
 
 
 _lib = None

@@ -14,7 +14,7 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-DEVICE_LIB = os.path.join(PKG_DIR, "libpnrt.so")
+DEVICE_LIB = os.environ.get("PNRT_DEVICE_LIB") or os.path.join(PKG_DIR, "libpnrt.so")
 HOST_LIB = os.path.join(PKG_DIR, "libpnrt_host.so")
 
 _cache: dict[str, ctypes.CDLL] = {}
@@ -87,6 +87,13 @@ class DeviceInfo(ctypes.Structure):
                 ("root_is_leaf", ctypes.c_int), ("stack_limit", ctypes.c_int)]
 
 
+K_CLASSES = ("primary", "gen", "setup", "trace", "shade", "blend", "v1")   # PNRT_K_* order
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double * len(K_CLASSES)), ("launches", ctypes.c_int64 * len(K_CLASSES))]
+
+
 def _sig(lib, name, res, *args):
     fn = getattr(lib, name)
     fn.restype = res
@@ -132,6 +139,8 @@ def _type_device(lib):
     _sig(lib, "pnrt_synchronize", INT, P)
     _sig(lib, "pnrt_get_device_info", INT, P, ctypes.POINTER(DeviceInfo))
     _sig(lib, "pnrt_debug_math", INT, P, INT, F, F, F, INT)
+    _sig(lib, "pnrt_profile_enable", INT, P, INT)
+    _sig(lib, "pnrt_profile_read", INT, P, ctypes.POINTER(Profile))
 
 
 def fptr(a) -> ctypes.POINTER(ctypes.c_float):

@@ -83,6 +83,12 @@ struct pnrt_ctx {
     void* wf = nullptr;         size_t wf_cap = 0;
     uint2* wf_ovf = nullptr;    size_t wf_ovf_cap = 0;
     int trace_grid = 0;
+    // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
+    bool prof_on = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+    double prof_ms[PNRT_K_COUNT] = {};
+    int64_t prof_n[PNRT_K_COUNT] = {};
     bool debug_simple_trace = false;
     int debug_variant = 0;
 };
@@ -97,6 +103,41 @@ static int set_err(pnrt_ctx* c, int code, const std::string& m) {
         if (e_ != hipSuccess)                                                                     \
             return set_err(ctx, PNRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
     } while (0)
+
+// ---- event timing: a start/stop event pair around every launch of a class ----------------
+static hipEvent_t ev_get(pnrt_ctx* c) {
+    if (!c->ev_pool.empty()) { hipEvent_t e = c->ev_pool.back(); c->ev_pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+struct ProfScope {     // records on the context stream, so it times exactly that stream's launches
+    pnrt_ctx* c; int k; hipEvent_t a = nullptr;
+    ProfScope(pnrt_ctx* c_, int k_) : c(c_), k(k_) {
+        if (c->prof_on && (a = ev_get(c))) (void)hipEventRecord(a, c->stream);
+    }
+    ~ProfScope() {
+        if (!a) return;
+        hipEvent_t b = ev_get(c);
+        if (!b) { c->ev_pool.push_back(a); return; }
+        (void)hipEventRecord(b, c->stream);
+        c->ev_pending.push_back({k, {a, b}});
+    }
+};
+static int prof_collect(pnrt_ctx* c) {
+    if (c->ev_pending.empty()) return PNRT_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto& p : c->ev_pending) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, p.second.first, p.second.second));
+        c->prof_ms[p.first] += ms;
+        c->prof_n[p.first] += 1;
+        c->ev_pool.push_back(p.second.first);
+        c->ev_pool.push_back(p.second.second);
+    }
+    c->ev_pending.clear();
+    return PNRT_OK;
+}
 
 #define WF_MAX_CHUNK_FRAMES 8
 
@@ -152,8 +193,11 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 4096)) ||
         (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * WF_OVF * 8)))
         return rc;
-    hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, s, fp,
-                       c->primary);
+    {
+        ProfScope ps(c, PNRT_K_PRIMARY);
+        hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, s, fp,
+                           c->primary);
+    }
     HIPCHK(c, hipGetLastError());
     for (uint32_t f0 = 0; f0 < nf; f0 += chunk) {
         uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
@@ -174,20 +218,30 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         b.tiles_x = tiles_x;
         b.first_frame = first + f0;
         const dim3 g((unsigned)((n + 255) / 256));
-        hipLaunchKernelGGL(pt_wf_gen, g, dim3(256), 0, c->stream, fp, b, (const float4*)c->primary, c->colors);
+        {
+            ProfScope ps(c, PNRT_K_GEN);
+            hipLaunchKernelGGL(pt_wf_gen, g, dim3(256), 0, c->stream, fp, b, (const float4*)c->primary, c->colors);
+        }
         HIPCHK(c, hipGetLastError());
         for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
-            hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
+            {
+                ProfScope ps(c, PNRT_K_SETUP);
+                hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
+            }
             HIPCHK(c, hipMemsetAsync(b.counter, 0, 4, c->stream));
-            if (c->debug_simple_trace)
-                hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b,
-                                   fp.mode);
-            else if (c->debug_variant == 1)   // deep LDS stack, no spill
-                hipLaunchKernelGGL((pt_wf_trace<48, false>), dim3(256), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
-            else if (c->debug_variant == 2)   // refill only when every lane is idle
-                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
-            else
-                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            {
+                ProfScope ps(c, PNRT_K_TRACE);
+                if (c->debug_simple_trace)
+                    hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b,
+                                       fp.mode);
+                else if (c->debug_variant == 1)   // deep LDS stack, no spill
+                    hipLaunchKernelGGL((pt_wf_trace<48, false>), dim3(256), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+                else if (c->debug_variant == 2)   // refill only when every lane is idle
+                    hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+                else
+                    hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+            }
+            HIPCHK(c, hipGetLastError());
             if (c->debug_variant == 9) {   // compare every ray with the simple kernel
                 std::vector<int> h1(n), h2(n);
                 std::vector<uint8_t> o1(2 * n), o2(2 * n);
@@ -214,11 +268,17 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
                 if (first[2] >= 0) fprintf(stderr, " cont p%ld persistent=%d simple=%d", first[2], h1[first[2]], h2[first[2]]);
                 fprintf(stderr, "\n");
             }
-            hipLaunchKernelGGL(pt_wf_shade, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
+            {
+                ProfScope ps(c, PNRT_K_SHADE);
+                hipLaunchKernelGGL(pt_wf_shade, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
+            }
             HIPCHK(c, hipGetLastError());
         }
-        hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
-                           (const float4*)c->colors, c->accum, (int)cf, first + f0);
+        {
+            ProfScope ps(c, PNRT_K_BLEND);
+            hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
+                               (const float4*)c->colors, c->accum, (int)cf, first + f0);
+        }
         HIPCHK(c, hipGetLastError());
     }
     return PNRT_OK;
@@ -274,6 +334,8 @@ void pnrt_destroy(pnrt_ctx* c) {
     (void)hipFree(c->accum);
     (void)hipFree(c->primary); (void)hipFree(c->colors);
     (void)hipFree(c->wf); (void)hipFree(c->wf_ovf);
+    for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -516,7 +578,10 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
     s.unorm8 = c->unorm8;
     if (c->kernel == 1) {
         dim3 grid((c->width + 15) / 16, (fp.rows + 15) / 16);
-        hipLaunchKernelGGL(pt_render_kernel, grid, dim3(256), 0, c->stream, s, fp, c->accum);
+        {
+            ProfScope ps(c, PNRT_K_V1);
+            hipLaunchKernelGGL(pt_render_kernel, grid, dim3(256), 0, c->stream, s, fp, c->accum);
+        }
         HIPCHK(c, hipGetLastError());
         return PNRT_OK;
     }
@@ -542,6 +607,24 @@ int pnrt_read_accum(pnrt_ctx* c, float* out) {
 }
 
 void* pnrt_accum_device_ptr(pnrt_ctx* c) { return c ? c->accum : nullptr; }
+
+int pnrt_profile_enable(pnrt_ctx* c, int on) {
+    if (!c) return PNRT_E_ARG;
+    int rc = prof_collect(c);
+    if (rc) return rc;
+    c->prof_on = on != 0;
+    for (int k = 0; k < PNRT_K_COUNT; ++k) { c->prof_ms[k] = 0.0; c->prof_n[k] = 0; }
+    return PNRT_OK;
+}
+
+int pnrt_profile_read(pnrt_ctx* c, pnrt_profile* out) {
+    if (!c || !out) return PNRT_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = prof_collect(c);
+    if (rc) return rc;
+    for (int k = 0; k < PNRT_K_COUNT; ++k) { out->ms[k] = c->prof_ms[k]; out->launches[k] = c->prof_n[k]; }
+    return PNRT_OK;
+}
 
 int pnrt_pack_rows(pnrt_ctx* c, void* dst, int band, int nsh, int shard) {
     if (!c || !dst) return PNRT_E_ARG;

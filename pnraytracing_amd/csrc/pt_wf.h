@@ -270,8 +270,11 @@ PN_DEV bool wf_load_ray(const DevScene& s, const WfBufs& b, uint32_t id, int mod
 // structured and loop-free inside a lane's step (one triangle test, one node,
 // or one stack pop per iteration) with every wave-level decision (ballot) at a
 // reconvergence point: the ray <-> lane refill runs once per outer iteration.
+#ifndef WF_TRACE_WAVES
+#define WF_TRACE_WAVES 1      // minimum waves per SIMD requested from the register allocator
+#endif
 template <int STK, bool SYNC>
-__global__ void __launch_bounds__(WF_TRACE_BLOCK) pt_wf_trace(DevScene s, WfBufs b, int mode) {
+__global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
     const int tl = threadIdx.x, lane = tl & 63;
     const uint32_t n_rays = 3u * b.n;

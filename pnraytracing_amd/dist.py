@@ -1,0 +1,77 @@
+"""Multi-GPU row-band sharding of one frame.
+
+Every pixel of ``ray_tracing.comp`` is independent -- the seed (``:977-979``)
+and the Cranley-Patterson shift (``:540-543``) depend only on (x, y, frame) --
+so any row partition reproduces the single-GPU image bit for bit.  Rank r of
+N renders the rows ``{y : (y // band) % N == r}`` (interleaved 8-row bands
+balance the expensive middle of the frame), packs them into a contiguous
+buffer and one ``gather`` (RCCL over xGMI for CUDA tensors, gloo on CPU)
+brings them to rank 0, which scatters them back into image order.  There is
+no other collective: the ranks never exchange data while rendering.
+
+One process per GPU (``torch.distributed.run``); the tracer of each rank
+must launch on the stream torch uses for the collective, which
+:class:`ShardedFrame` arranges for CUDA devices.
+
+The tracer protocol is the one of :class:`pnraytracing_amd.tracer.PathTracer`:
+``width``, ``height``, ``render(first, n, band, n_shards, shard)`` and
+``pack_rows(dst_ptr, band, n_shards, shard)``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .tracer import shard_rows
+
+BAND = 8
+
+
+class ShardedFrame:
+    """Render the rows of this rank and gather the frame to rank 0."""
+
+    def __init__(self, tracer, band: int = BAND, device: str | torch.device = "cuda", group=None):
+        self.tracer, self.band, self.group = tracer, band, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.device = torch.device(device)
+        H, W = tracer.height, tracer.width
+        if H <= 0 or W <= 0:
+            raise ValueError("ShardedFrame: set_frame() the tracer first")
+        rows = [shard_rows(H, band, self.world, r) for r in range(self.world)]
+        self.rows = [torch.as_tensor(r, device=self.device) for r in rows]
+        self.my_rows = len(rows[self.rank])
+        self.max_rows = max(len(r) for r in rows)           # rank 0 owns the most (first bands)
+        # equal-sized buffers for the collective; the tail of a short shard is padding
+        self.send = torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=self.device)
+        self.recv = [torch.zeros_like(self.send) for _ in range(self.world)] if self.rank == 0 else None
+        self.image = torch.zeros((H, W, 4), dtype=torch.float32, device=self.device) if self.rank == 0 else None
+        if self.device.type == "cuda" and hasattr(tracer, "set_stream"):
+            tracer.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def render(self, first_frame: int, n_frames: int):
+        """Asynchronously render frames first..first+n-1 of this rank's rows."""
+        self.tracer.render(first_frame, n_frames, self.band, self.world, self.rank)
+
+    def gather(self) -> torch.Tensor | None:
+        """Pack this rank's rows, gather on rank 0; returns the H x W x 4 image
+        (row 0 = bottom) on rank 0 and None elsewhere."""
+        if self.my_rows:
+            self.tracer.pack_rows(self.send.data_ptr(), self.band, self.world, self.rank)
+        if self.world == 1:
+            self.image.copy_(self.send)
+            return self.image
+        dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0, group=self.group)
+        if self.rank != 0:
+            return None
+        for r in range(self.world):
+            n = len(self.rows[r])
+            if n:
+                self.image.index_copy_(0, self.rows[r], self.recv[r][:n])
+        return self.image
+
+
+def row_owner(height: int, band: int, world: int) -> np.ndarray:
+    """Rank that owns each row (for tests and tools)."""
+    return (np.arange(height) // band) % world

@@ -119,6 +119,16 @@ class PathTracer:
         self._ck(self._lib.pnrt_get_device_info(self._ctx, ctypes.byref(info)), "pnrt_get_device_info")
         return {f: getattr(info, f) for f, _ in info._fields_}
 
+    def profile_enable(self, on: bool = True):
+        """Bracket every kernel launch with HIP events on the launch stream (resets totals)."""
+        self._ck(self._lib.pnrt_profile_enable(self._ctx, int(bool(on))), "pnrt_profile_enable")
+
+    def profile_read(self) -> dict:
+        """{kernel class: (total ms, launches)} since profile_enable (synchronises)."""
+        p = N.Profile()
+        self._ck(self._lib.pnrt_profile_read(self._ctx, ctypes.byref(p)), "pnrt_profile_read")
+        return {k: (p.ms[i], int(p.launches[i])) for i, k in enumerate(N.K_CLASSES)}
+
     def debug_math(self, fn: int, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:
         a = np.ascontiguousarray(a, np.float32)
         b = None if b is None else np.ascontiguousarray(b, np.float32)
