@@ -186,11 +186,11 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
-    const size_t per_path = 16 * 12 + 4 + 4 + 2;      // S0-5, C0-3, R0-1 | flags | hit | occ
+    const size_t per_path = 16 * 12 + 4 + 4 + 2 + 12 + 1;  // S0-5, C0-3, R0-1 | flags | hit | occ | ray queues | counts
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 4096)) ||
+        (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 8192)) ||
         (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * WF_OVF * 8)))
         return rc;
     {
@@ -211,7 +211,14 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         b.hit = reinterpret_cast<int*>(base + off); off += n * 4;
         b.occ = reinterpret_cast<uint8_t*>(base + off); off += n * 2;
         off = (off + 255) & ~(size_t)255;
-        b.counter = reinterpret_cast<unsigned int*>(base + off); off += 256;
+        b.npad = (uint32_t)((n + 255) / 256 * 256);
+        b.nseg_k = b.npad / 256;
+        b.rayq = reinterpret_cast<uint32_t*>(base + off); off += (size_t)b.npad * 12;
+        b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
+        off = (off + 255) & ~(size_t)255;
+        off = (off + 255) & ~(size_t)255;
+        b.counter = reinterpret_cast<unsigned int*>(base + off);
+        b.stats = reinterpret_cast<unsigned long long*>(base + off + 64); off += 256;
         b.ovf = c->wf_ovf;
         b.n = (uint32_t)n;
         b.chunk_frames = (int)cf;
@@ -224,11 +231,12 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         }
         HIPCHK(c, hipGetLastError());
         for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
+            // segment dequeue counter (+ the WF_STATS census)
+            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 4, c->stream));
             {
                 ProfScope ps(c, PNRT_K_SETUP);
                 hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
             }
-            HIPCHK(c, hipMemsetAsync(b.counter, 0, 4, c->stream));
             {
                 ProfScope ps(c, PNRT_K_TRACE);
                 if (c->debug_simple_trace)
@@ -242,6 +250,14 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
                     hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
             }
             HIPCHK(c, hipGetLastError());
+            if (WF_STATS) {
+                unsigned long long st[8];
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+                HIPCHK(c, hipMemcpy(st, b.stats, sizeof st, hipMemcpyDeviceToHost));
+                fprintf(stderr, "[trace stats] bounce %d n=%zu iters=%llu active/iter=%.1f tri=%llu pop=%llu node=%llu "
+                        "refills=%llu rays=%llu  lane-steps/ray=%.1f\n", bounce, n, st[0], st[0] ? (double)st[1] / st[0] : 0.0,
+                        st[2], st[3], st[4], st[5], st[6], st[6] ? (double)st[1] / st[6] : 0.0);
+            }
             if (c->debug_variant == 9) {   // compare every ray with the simple kernel
                 std::vector<int> h1(n), h2(n);
                 std::vector<uint8_t> o1(2 * n), o2(2 * n);

@@ -19,29 +19,28 @@
 // ---- ray with per-ray precomputation ------------------------------------------------
 struct RayP {
     f3 o, d;
-    f3 inv;           // 1/dir (BoundIntersect :214); also the triangle test's invDz
-    int kx, ky, kz;   // triangle-test axis permutation (:269-282)
-    float sx, sy, invDz;
-    bool cull_ok;     // z-slab culling is provably result-neutral for this ray
+    f3 inv;           // 1/dir (BoundIntersect :214); inv[kz] is the triangle test's invDz
+    int perm;         // bits 0-1: kz of the axis permutation (:269-282; 2 = identity),
+                      // bit 2: z-slab culling is provably result-neutral for this ray
+    PN_DEV int kz() const { return perm & 3; }
+    PN_DEV int kx() const { return (perm & 3) == 0 ? 2 : 0; }   // kz = 0: x <-> z swapped
+    PN_DEV int ky() const { return (perm & 3) == 1 ? 2 : 1; }   // kz = 1: y <-> z swapped
+    PN_DEV bool cull_ok() const { return (perm & 4) != 0; }
 };
 
 PN_DEV RayP make_ray(f3 o, f3 d, int mode) {
     RayP r;
     r.o = o; r.d = d;
     r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    r.kx = 0; r.ky = 1; r.kz = 2;
-    if (d.z == 0.0f) {
-        if (pnm_fabs(d.x) > pnm_fabs(d.y)) { r.kx = 2; r.kz = 0; }
-        else { r.ky = 2; r.kz = 1; }
-    }
-    float dz = comp(d, r.kz);
-    r.sx = comp(d, r.kx); r.sy = comp(d, r.ky);
-    r.invDz = 1.0f / dz;
+    int kz = 2;
+    if (d.z == 0.0f) kz = (pnm_fabs(d.x) > pnm_fabs(d.y)) ? 0 : 1;
+    float dz = comp(d, kz);
     // z-slab culling needs finite rays and a non-tiny z so no sheared
     // coordinate can overflow into NaN edge functions (Culling).
     bool fin = pnm_fabs(o.x) < 1e6f && pnm_fabs(o.y) < 1e6f && pnm_fabs(o.z) < 1e6f &&
                pnm_fabs(d.x) < 1e6f && pnm_fabs(d.y) < 1e6f && pnm_fabs(d.z) < 1e6f;
-    r.cull_ok = (mode != 0) && fin && pnm_fabs(dz) >= 1e-12f;
+    bool cull = (mode != 0) && fin && pnm_fabs(dz) >= 1e-12f;
+    r.perm = kz | (cull ? 4 : 0);
     return r;
 }
 
@@ -55,8 +54,9 @@ PN_DEV bool box_test(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     float tminx = fmin_(fx, nx), tminy = fmin_(fy, ny), tminz = fmin_(fz, nz);
     float t1 = fmin_(tmaxx, fmin_(tmaxy, tmaxz));
     float t0 = fmax_(tminx, fmax_(tminy, tminz));
-    float zf = r.kz == 2 ? fz : (r.kz == 0 ? fx : fy);
-    float zn = r.kz == 2 ? nz : (r.kz == 0 ? nx : ny);
+    const int kz = r.kz();
+    float zf = kz == 2 ? fz : (kz == 0 ? fx : fy);
+    float zn = kz == 2 ? nz : (kz == 0 ? nx : ny);
     zlo = zn < zf ? zn : zf;   // NaN -> comparisons below fail -> never culled
     zhi = zn < zf ? zf : zn;
     return t1 >= t0;
@@ -65,20 +65,26 @@ PN_DEV bool box_test(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 // Culling predicate: every triangle inside a box with this z-slab is rejected by
 // the watertight test at the current tMax (proof in DESIGN.md, "Culling").
 PN_DEV bool zcull(const RayP& r, float zlo, float zhi, float tmax_c) {
-    return r.cull_ok && (zhi <= 0.0f || (zlo > tmax_c && zlo > 1e-20f));
+    return r.cull_ok() && (zhi <= 0.0f || (zlo > tmax_c && zlo > 1e-20f));
 }
 
-// Watertight triangle test front half (:254-318 / :360-424).
+// Watertight triangle test front half (:254-318 / :360-424).  IDENT: the
+// caller guarantees the permutation is the identity (kz = 2, i.e. rd.z != 0),
+// which skips the component selects; the arithmetic is the same.
+template <bool IDENT = false>
 PN_DEV bool tri_test(const RayP& r, const float4& t0, const float4& t1, const float4& t2,
                      float tMax, float& e0o, float& e1o, float& e2o, float& deto, float& tso) {
     f3 p0 = mk3(t0.x, t0.y, t0.z), p1 = mk3(t0.w, t1.x, t1.y), p2 = mk3(t1.z, t1.w, t2.x);
     f3 P0 = sub(p0, r.o), P1 = sub(p1, r.o), P2 = sub(p2, r.o);
-    float P0x = comp(P0, r.kx), P0y = comp(P0, r.ky), P0z = comp(P0, r.kz);
-    float P1x = comp(P1, r.kx), P1y = comp(P1, r.ky), P1z = comp(P1, r.kz);
-    float P2x = comp(P2, r.kx), P2y = comp(P2, r.ky), P2z = comp(P2, r.kz);
-    P0x = P0x - (P0z * r.sx) * r.invDz; P0y = P0y - (P0z * r.sy) * r.invDz; P0z = P0z * r.invDz;
-    P1x = P1x - (P1z * r.sx) * r.invDz; P1y = P1y - (P1z * r.sy) * r.invDz; P1z = P1z * r.invDz;
-    P2x = P2x - (P2z * r.sx) * r.invDz; P2y = P2y - (P2z * r.sy) * r.invDz; P2z = P2z * r.invDz;
+    const int kx = IDENT ? 0 : r.kx(), ky = IDENT ? 1 : r.ky(), kz = IDENT ? 2 : r.kz();
+    float P0x = comp(P0, kx), P0y = comp(P0, ky), P0z = comp(P0, kz);
+    float P1x = comp(P1, kx), P1y = comp(P1, ky), P1z = comp(P1, kz);
+    float P2x = comp(P2, kx), P2y = comp(P2, ky), P2z = comp(P2, kz);
+    // Sx = dir[kx]/dir[kz], written as the reference's (P.z * dir[kx]) * invDz
+    const float sx = comp(r.d, kx), sy = comp(r.d, ky), invDz = comp(r.inv, kz);
+    P0x = P0x - (P0z * sx) * invDz; P0y = P0y - (P0z * sy) * invDz; P0z = P0z * invDz;
+    P1x = P1x - (P1z * sx) * invDz; P1y = P1y - (P1z * sy) * invDz; P1z = P1z * invDz;
+    P2x = P2x - (P2z * sx) * invDz; P2y = P2y - (P2z * sy) * invDz; P2z = P2z * invDz;
     float e0 = P1x * P2y - P1y * P2x;
     float e1 = P2x * P0y - P2y * P0x;
     float e2 = P0x * P1y - P0y * P1x;
@@ -157,7 +163,7 @@ PN_DEV bool traverse(const DevScene& s, const RayP& r, float& tMax, int& hitTri)
             if (sp == 0) return hit;
             --sp;
             cur = stackRef[sp];
-            if (!(r.cull_ok && stackZ[sp] > tMax * cullScale && stackZ[sp] > 1e-20f)) break;
+            if (!(r.cull_ok() && stackZ[sp] > tMax * cullScale && stackZ[sp] > 1e-20f)) break;
         }
     }
 }

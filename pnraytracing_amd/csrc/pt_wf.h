@@ -12,6 +12,7 @@
 //             hit (emission, throughput), next bounce or the final colour
 // so each kernel is compact and coherent instead of one 240-VGPR megakernel.
 #pragma once
+#include <type_traits>
 #include "pt_passes.h"
 
 #define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
@@ -46,7 +47,15 @@ struct WfBufs {
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
     uint2* ovf;        // traversal stack spill
-    unsigned int* counter;   // ray dequeue counter (zeroed before each trace launch)
+    unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
+    // ray queues, written by setup without atomics: setup block j compacts its
+    // paths' rays of kind k into segment (k, j) = rayq[k * npad + 256 j ...]
+    // and stores the count in segcount[k * nseg_k + j]
+    uint32_t* rayq;          // [3 * npad] path slots
+    unsigned int* segcount;  // [3 * nseg_k]
+    uint32_t npad;           // n rounded up to 256
+    uint32_t nseg_k;         // setup blocks = segments per kind
+    unsigned long long* stats; // WF_STATS builds: traversal step census (8 counters)
     uint32_t n;        // path slots
     int chunk_frames;
     int tiles_x;
@@ -97,11 +106,7 @@ __global__ void __launch_bounds__(256) pt_wf_gen(FrameParams fp, WfBufs b, const
 }
 
 // ---- setup: one bounce's sampling and BRDF values (ray_tracing.comp:866-934) -----------------
-__global__ void __launch_bounds__(256) pt_wf_setup(DevScene s, FrameParams fp, WfBufs b) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
-    uint32_t fl = b.flags[i];
-    if (!(fl & WF_ALIVE)) return;
+PN_DEV uint32_t wf_setup_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t fl) {
     const int bounce = (int)((fl >> 8) & 7u);
     int x, lr, k;
     wf_coords(b, i, x, lr, k);
@@ -217,9 +222,56 @@ __global__ void __launch_bounds__(256) pt_wf_setup(DevScene s, FrameParams fp, W
     b.C3[i] = make_float4(L.x, L.y, L.z, dPDF);
     b.S3[i] = make_float4(s3.x, s3.y, s3.z, __uint_as_float(seed));
     b.flags[i] = nfl | WF_RCONT;
+    return nfl | WF_RCONT;
+}
+
+// Compact the block's rays of each kind into its own queue segment: a ballot
+// per wave, wave offsets through LDS, no global atomics.  Each ray's traversal
+// result is independent of every other ray and of its queue position.
+PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl) {
+    __shared__ unsigned int wcnt[3][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t need[3] = {WF_RLIGHT, WF_RENV, WF_RCONT};
+    uint64_t m[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        m[k] = __ballot((nfl & need[k]) != 0);
+        if (lane == 0) wcnt[k][wave] = (unsigned int)__popcll(m[k]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned int off = 0;
+        for (int w = 0; w < wave; ++w) off += wcnt[k][w];
+        if (nfl & need[k])
+            b.rayq[(size_t)k * b.npad + (size_t)blockIdx.x * 256 + off + (uint32_t)__popcll(m[k] & lt_mask)] = i;
+    }
+    if (threadIdx.x < 3)
+        b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] =
+            wcnt[threadIdx.x][0] + wcnt[threadIdx.x][1] + wcnt[threadIdx.x][2] + wcnt[threadIdx.x][3];
+}
+
+__global__ void __launch_bounds__(256) pt_wf_setup(DevScene s, FrameParams fp, WfBufs b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nfl = 0;
+    if (i < b.n) {
+        const uint32_t fl = b.flags[i];
+        if (fl & WF_ALIVE) nfl = wf_setup_path(s, fp, b, i, fl);
+    }
+    wf_enqueue(b, i, nfl);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
+// Per-lane spill area of the traversal stack (address formed only when used).
+PN_DEV uint2* wf_ovf(const WfBufs& b, int tl) {
+    return b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * WF_OVF;
+}
+// Number of set bits of m below this lane (v_mbcnt).
+PN_DEV uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 template <int STK>
 PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, float z) {
     uint2 e = make_uint2(ref, __float_as_uint(z));
@@ -230,40 +282,67 @@ PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, flo
 template <int STK>
 PN_DEV uint2 wf_pop(const uint2* lds, const uint2* ovf, int lane, int& sp) {
     --sp;
-    return sp < STK ? lds[sp * WF_TRACE_BLOCK + lane] : ovf[sp - STK];
+    // unconditional LDS read + a rare global read (keeps the common pop a ds_read,
+    // not a flat load that would wait on every outstanding memory operation)
+    uint2 e = lds[(sp < STK ? sp : STK - 1) * WF_TRACE_BLOCK + lane];
+    if (sp >= STK) e = ovf[sp - STK];
+    return e;
 }
 
 // BoundIntersect (:213-228) for traversal decisions.  fminf/fmaxf (v_min/v_max)
 // drop NaNs exactly like the oracle's min/max; the results only feed
 // comparisons, where the sign of a zero cannot matter -> same booleans.
+template <bool IDENT = false>
 PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
                      float& zlo) {
     float fx = (mxx - r.o.x) * r.inv.x, fy = (mxy - r.o.y) * r.inv.y, fz = (mxz - r.o.z) * r.inv.z;
     float nx = (mnx - r.o.x) * r.inv.x, ny = (mny - r.o.y) * r.inv.y, nz = (mnz - r.o.z) * r.inv.z;
     float t1 = fminf(fmaxf(fx, nx), fminf(fmaxf(fy, ny), fmaxf(fz, nz)));
     float t0 = fmaxf(fminf(fx, nx), fmaxf(fminf(fy, ny), fminf(fz, nz)));
-    float zf = r.kz == 2 ? fz : (r.kz == 0 ? fx : fy);
-    float zn = r.kz == 2 ? nz : (r.kz == 0 ? nx : ny);
+    const int kz = IDENT ? 2 : r.kz();
+    float zf = kz == 2 ? fz : (kz == 0 ? fx : fy);
+    float zn = kz == 2 ? nz : (kz == 0 ? nx : ny);
     float lo = zn < zf ? zn : zf, hi = zn < zf ? zf : zn;
     zlo = lo;
     // zhi <= 0: the whole box is behind the ray in the triangle test's frame
-    return (t1 >= t0) && !(r.cull_ok && hi <= 0.0f);
+    return (t1 >= t0) && !(r.cull_ok() && hi <= 0.0f);
 }
 
-// Fetch ray `id` of the bounce into a lane (false if that ray does not exist).
-PN_DEV bool wf_load_ray(const DevScene& s, const WfBufs& b, uint32_t id, int mode, RayP& r, float& tmax, bool& any) {
-    uint32_t kind = id / b.n, p = id - kind * b.n;
-    uint32_t fl = b.flags[p];
-    uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
-    if (!((fl & WF_ALIVE) && (fl & need))) return false;
-    float4 s0 = b.S0[p], s1 = b.S1[p];
+#ifndef WF_TRI2
+#define WF_TRI2 0      // two triangle tests per traversal step
+#endif
+#ifndef WF_MERGE_POP
+#define WF_MERGE_POP 1 // a popped node is visited in the same step
+#endif
+#ifndef WF_STATS
+#define WF_STATS 0     // diagnostic builds: count iterations / lane steps per trace launch
+#endif
+#ifndef WF_NT
+#define WF_NT 0        // non-temporal path-state traffic in the trace kernel (keeps the BVH in L2)
+#endif
+template <typename T>
+PN_DEV T wf_ld(const T* a) {
+    if (WF_NT) return __builtin_nontemporal_load(a);
+    return *a;
+}
+PN_DEV float4 wf_ld4(const float4* a) {
+    if (WF_NT) {
+        const float* f = reinterpret_cast<const float*>(a);
+        return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1),
+                           __builtin_nontemporal_load(f + 2), __builtin_nontemporal_load(f + 3));
+    }
+    return *a;
+}
+
+// Load ray (kind, path p) of the bounce into a lane.
+PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t p, int mode, RayP& r, float& tmax, bool& any) {
+    float4 s0 = wf_ld4(b.S0 + p), s1 = wf_ld4(b.S1 + p);
     f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
-    float4 dv = kind == 0 ? b.R0[p] : (kind == 1 ? b.R1[p] : b.C3[p]);
+    float4 dv = wf_ld4(kind == 0 ? b.R0 + p : (kind == 1 ? b.R1 + p : b.C3 + p));
     f3 o = kind == 1 ? P : add(P, muls(N, 0.0001f));
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
     r = make_ray(o, mk3(dv.x, dv.y, dv.z), mode);
-    return true;
 }
 
 // Persistent traversal of every ray of the bounce.  Control flow is kept
@@ -277,13 +356,11 @@ template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
     const int tl = threadIdx.x, lane = tl & 63;
-    const uint32_t n_rays = 3u * b.n;
-    // rays are dequeued in chunks of WF_CHUNK consecutive ids (kind-major order, so
-    // a chunk's rays share a kind and neighbouring pixels); one atomic per chunk
-    uint32_t next = 0, end = 0;
+    // rays are dequeued one queue segment at a time (<= 256 rays of one kind from
+    // 256 neighbouring paths, kind-major); one atomic per segment
+    const uint32_t nseg = 3u * b.nseg_k;
+    uint32_t next = 0, end = 0, ckind = 0;
     bool exhausted = false;
-    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    uint2* ovf = b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * WF_OVF;
 
     RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
     float tMax = 0.f;
@@ -291,39 +368,54 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     uint32_t cur = REF_NONE, rid = 0;
     bool any = true;
     int busy = 0;
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, pop, node, refill, rays, -
 
     for (;;) {
-        // ---- refill (one pass): idle lanes take the wave's next ray ids -------------------
-        const uint64_t idle = __ballot(busy == 0);
-        if (idle != 0 && next >= end && !exhausted) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(b.counter, WF_CHUNK);
-            base = __shfl(base, 0);
-            if (base >= n_rays) exhausted = true;
-            else { next = base; end = min(base + WF_CHUNK, n_rays); }
-        }
-        if (idle != 0 && next < end) {
-            const uint32_t myid = next + (uint32_t)__popcll(idle & lt_mask);
-            next = min(next + (uint32_t)__popcll(idle), end);
-            if (busy == 0 && myid < end) {
-                RayP nr;
-                float ntmax;
-                bool nany;
-                if (wf_load_ray(s, b, myid, mode, nr, ntmax, nany)) {
-                    float zlo;
-                    uint32_t root = REF_NONE;
-                    int nlt = 0, nlc = 0;
-                    if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
-                                 s.root_max[2], zlo)) {
-                        root = s.root_ref;
-                        if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
-                    }
-                    r = nr; tMax = ntmax; any = nany; rid = myid;
-                    hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
-                    busy = 1;
+        // ---- refill: idle lanes take the wave's next queued rays; more passes when a
+        // segment runs out part-way (wave-uniform control flow only)
+        const int busy0 = WF_STATS ? __popcll(__ballot(busy != 0)) : 0;
+        auto refill = [&]() {
+            const uint64_t idle = __ballot(busy == 0);
+            if (idle != 0 && next >= end && !exhausted) {
+                uint32_t seg = 0;
+                if (lane == 0) seg = atomicAdd(b.counter, 1u);
+                seg = __builtin_amdgcn_readfirstlane(seg);
+                if (seg >= nseg) exhausted = true;
+                else {
+                    ckind = seg / b.nseg_k;
+                    const uint32_t j = seg - ckind * b.nseg_k;
+                    next = ckind * b.npad + j * 256u;
+                    end = next + b.segcount[seg];
                 }
             }
-        }
+            if (idle != 0 && next < end) {
+                const uint32_t myid = next + lanes_below(idle);
+                next = min(next + (uint32_t)__popcll(idle), end);
+                if (busy == 0 && myid < end) {
+                    RayP nr;
+                    float ntmax;
+                    bool nany;
+                    {
+                        const uint32_t kind = ckind;
+                        const uint32_t p = b.rayq[myid];
+                        wf_load_ray(b, kind, p, mode, nr, ntmax, nany);
+                        float zlo;
+                        uint32_t root = REF_NONE;
+                        int nlt = 0, nlc = 0;
+                        if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                                     s.root_max[2], zlo)) {
+                            root = s.root_ref;
+                            if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
+                        }
+                        r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
+                        hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
+                        busy = 1;
+                    }
+                }
+            }
+        };
+        for (int pass = 0; pass < 4 && !exhausted && __ballot(busy == 0) != 0; ++pass) refill();
+        if (WF_STATS) { st[5] += 1; st[6] += __popcll(__ballot(busy != 0)) - busy0; }
         const uint64_t busym = __ballot(busy != 0);
         if (busym == 0) {
             if (exhausted) break;
@@ -331,61 +423,100 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         }
         const int thr = SYNC ? 0 : __popcll(busym) / 2;
         // ---- traverse until half of the lanes have finished their ray ------------------
+        // (IDENT: no lane of the wave needs the triangle test's axis permutation)
+        auto run = [&](auto ident_tag) {
+        constexpr bool ID = decltype(ident_tag)::value;
         for (;;) {
+            if (WF_STATS) {
+                st[0] += 1;
+                st[1] += __popcll(__ballot(busy != 0));
+                st[2] += __popcll(__ballot(busy != 0 && lc > 0));
+                st[3] += __popcll(__ballot(busy != 0 && lc <= 0 && cur == REF_NONE && sp > 0));
+                st[4] += __popcll(__ballot(busy != 0 && lc <= 0 && (cur != REF_NONE || (WF_MERGE_POP && sp > 0))));
+            }
             if (busy) {
                 bool done = false;
+                bool popped_this_step = cur == REF_NONE;
                 if (lc > 0) {
+                    // one triangle per step, or two (WF_TRI2): both records are
+                    // loaded up front, tested in BVH order (the second sees the
+                    // tMax the first may have set; any-hit stops at the first)
                     const float4* tp = s.tris + 3 * (size_t)lt;
+                    const bool two = WF_TRI2 && lc >= 2;
+                    float4 q0 = tp[0], q1 = tp[1], q2 = tp[2], q3, q4, q5;
+                    if (two) { q3 = tp[3]; q4 = tp[4]; q5 = tp[5]; }
                     float e0, e1, e2, det, ts;
-                    if (tri_test(r, tp[0], tp[1], tp[2], tMax, e0, e1, e2, det, ts)) {
+                    if (tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts)) {
                         hitTri = lt;
                         if (any) done = true;
                         else tMax = ts * (1.0f / det);
                     }
                     ++lt; --lc;
-                } else if (cur == REF_NONE) {
-                    if (sp == 0) {
-                        done = true;
-                    } else {
-                        uint2 e = wf_pop<STK>(lds, ovf, tl, sp);
-                        float z = __uint_as_float(e.y);
-                        bool culled = r.cull_ok && z > tMax * 1.000001f && z > 1e-20f;
-                        if (!culled) {
-                            if (e.x & REF_LEAF) decode_leaf(s, e.x, lt, lc);
-                            else cur = e.x;
+                    if (two && !done) {
+                        if (tri_test<ID>(r, q3, q4, q5, tMax, e0, e1, e2, det, ts)) {
+                            hitTri = lt;
+                            if (any) done = true;
+                            else tMax = ts * (1.0f / det);
                         }
+                        ++lt; --lc;
                     }
                 } else {
-                    const float4* nd = s.nodes + 4 * (size_t)cur;
-                    float4 a = nd[0], bb = nd[1], c = nd[2];
-                    uint4 m = *reinterpret_cast<const uint4*>(nd + 3);
-                    const float tmc = tMax * 1.000001f;
-                    float zloL, zloR;
-                    bool hL = box_fast(r, a.x, a.y, a.z, a.w, bb.x, bb.y, zloL);
-                    bool hR = box_fast(r, bb.z, bb.w, c.x, c.y, c.z, c.w, zloR);
-                    if (r.cull_ok) {
-                        if (zloL > tmc && zloL > 1e-20f) hL = false;
-                        if (zloR > tmc && zloR > 1e-20f) hR = false;
+                    if (cur == REF_NONE) {
+                        if (sp == 0) {
+                            done = true;
+                        } else {
+                            uint2 e = wf_pop<STK>(lds, wf_ovf(b, tl), tl, sp);
+                            float z = __uint_as_float(e.y);
+                            bool culled = r.cull_ok() && z > tMax * 1.000001f && z > 1e-20f;
+                            if (!culled) {
+                                if (e.x & REF_LEAF) decode_leaf(s, e.x, lt, lc);
+                                else cur = e.x;
+                            }
+                        }
                     }
-                    bool rightFirst = comp(r.d, (int)m.z) < 0;     // :448
-                    uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
-                    bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
-                    float zFar = rightFirst ? zloL : zloR;
-                    if (hNear && hFar) wf_push<STK>(lds, ovf, tl, sp, farRef, zFar);
-                    uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
-                    if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
-                    cur = go;
+                    // WF_MERGE_POP: a popped interior node is visited in the same step
+                    if (cur != REF_NONE && (WF_MERGE_POP || !popped_this_step)) {
+                        const float4* nd = s.nodes + 4 * (size_t)cur;
+                        float4 a = nd[0], bb = nd[1], c = nd[2];
+                        uint4 m = *reinterpret_cast<const uint4*>(nd + 3);
+                        const float tmc = tMax * 1.000001f;
+                        float zloL, zloR;
+                        bool hL = box_fast<ID>(r, a.x, a.y, a.z, a.w, bb.x, bb.y, zloL);
+                        bool hR = box_fast<ID>(r, bb.z, bb.w, c.x, c.y, c.z, c.w, zloR);
+                        if (r.cull_ok()) {
+                            if (zloL > tmc && zloL > 1e-20f) hL = false;
+                            if (zloR > tmc && zloR > 1e-20f) hR = false;
+                        }
+                        bool rightFirst = comp(r.d, (int)m.z) < 0;     // :448
+                        uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+                        bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+                        float zFar = rightFirst ? zloL : zloR;
+                        if (hNear && hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
+                        uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
+                        if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
+                        cur = go;
+                    }
                 }
                 if (done) {
-                    uint32_t kind = rid / b.n, p = rid - kind * b.n;
-                    if (kind == 2) b.hit[p] = hitTri;
-                    else b.occ[2 * (size_t)p + kind] = hitTri >= 0 ? 1 : 0;
+                    const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
+                    if (WF_NT) {
+                        if (kind == 2) __builtin_nontemporal_store(hitTri, b.hit + p);
+                        else __builtin_nontemporal_store((uint8_t)(hitTri >= 0 ? 1 : 0), b.occ + 2 * (size_t)p + kind);
+                    } else {
+                        if (kind == 2) b.hit[p] = hitTri;
+                        else b.occ[2 * (size_t)p + kind] = hitTri >= 0 ? 1 : 0;
+                    }
                     busy = 0;
                 }
             }
             if (__popcll(__ballot(busy != 0)) <= thr) break;
         }
+        };
+        if (__ballot(busy != 0 && r.kz() != 2) == 0) run(std::true_type{});
+        else run(std::false_type{});
     }
+    if (WF_STATS && lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd(b.stats + k, st[k]);
 }
 
 // ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
@@ -448,7 +579,7 @@ __global__ void __launch_bounds__(256) pt_wf_shade(DevScene s, FrameParams fp, W
 __global__ void __launch_bounds__(256) pt_wf_trace_simple(DevScene s, WfBufs b, int mode) {
     uint32_t myid = blockIdx.x * blockDim.x + threadIdx.x;
     if (myid >= 3u * b.n) return;
-    uint32_t kind = myid / b.n, p = myid - kind * b.n;
+    const uint32_t kind = myid / b.n, p = myid - kind * b.n;
     uint32_t fl = b.flags[p];
     uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
     if (!((fl & WF_ALIVE) && (fl & need))) return;

@@ -1,20 +1,18 @@
 #!/bin/bash
-# PMC passes (one counter group per rocprofv3 run, kernel-trace only, no sys/runtime trace).
+# PMC passes on the default library: one counter group per rocprofv3 run
+# (kernel-trace only, never combined with sys/runtime traces).
+#   tools/gpu_pmc.sh <groups-file> [out-dir]     (one group per line)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p gpurun_out/pmc
+OUT=${2:-gpurun_out/pmcdiag}
+mkdir -p $OUT
 export TMPDIR=/tmp
-rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
-ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline"}
 i=0
 while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  for v in ${VARIANTS:-v2 v1}; do
-    timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/pmc/p${i}_$v -o run --output-format csv -- \
-      python bench.py $ARGS --kernel $v > gpurun_out/pmc/p${i}_$v.log 2>&1
-    rc=$?; echo "pass $i [$grp] $v rc=$rc"
-    [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-  done
-done <<GROUPS
-${PMC_GROUPS}
-GROUPS
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d $OUT/p${i}_default -o run --output-format csv -- \
+    python bench.py $ARGS > $OUT/p${i}.log 2>&1
+  rc=$?; echo "pass $i [$grp] rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done < "$1"
+exit 0
