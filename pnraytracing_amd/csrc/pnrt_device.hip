@@ -83,6 +83,7 @@ struct pnrt_ctx {
     void* wf = nullptr;         size_t wf_cap = 0;
     uint2* wf_ovf = nullptr;    size_t wf_ovf_cap = 0;
     int trace_grid = 0;
+    int wf_stack_need = 0;                 // wide-traversal stack entries per lane (from upload)
     // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
     bool prof_on = false;
     std::vector<hipEvent_t> ev_pool;
@@ -186,12 +187,14 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
-    const size_t per_path = 16 * 12 + 4 + 4 + 2 + 12 + 1;  // S0-5, C0-3, R0-1 | flags | hit | occ | ray queues | counts
+    // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
+    const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
+    const size_t per_path = 16 * 11 + 4 + 4 + 2 + 24 + 1;  // S0-3,S5, C0-3, R0-1 | flags | hit | occ | ray + deferred queues | counts
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
         (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 8192)) ||
-        (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * WF_OVF * 8)))
+        (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8)))
         return rc;
     {
         ProfScope ps(c, PNRT_K_PRIMARY);
@@ -204,7 +207,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         WfBufs b;
         size_t n = (size_t)tiles_x * tiles_y * 64 * cf;
         char* base = static_cast<char*>(c->wf);
-        float4** f4[] = {&b.S0, &b.S1, &b.S2, &b.S3, &b.S4, &b.S5, &b.C0, &b.C1, &b.C2, &b.C3, &b.R0, &b.R1};
+        float4** f4[] = {&b.S0, &b.S1, &b.S2, &b.S3, &b.S5, &b.C0, &b.C1, &b.C2, &b.C3, &b.R0, &b.R1};
         size_t off = 0;
         for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
         b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
@@ -214,29 +217,29 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         b.npad = (uint32_t)((n + 255) / 256 * 256);
         b.nseg_k = b.npad / 256;
         b.rayq = reinterpret_cast<uint32_t*>(base + off); off += (size_t)b.npad * 12;
+        b.defq = reinterpret_cast<uint32_t*>(base + off); off += (size_t)b.npad * 12;
         b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
         off = (off + 255) & ~(size_t)255;
         off = (off + 255) & ~(size_t)255;
         b.counter = reinterpret_cast<unsigned int*>(base + off);
+        b.defcount = b.counter + 4;
         b.stats = reinterpret_cast<unsigned long long*>(base + off + 64); off += 256;
         b.ovf = c->wf_ovf;
+        b.ovf_stride = (uint32_t)ovf_stride;
         b.n = (uint32_t)n;
         b.chunk_frames = (int)cf;
         b.tiles_x = tiles_x;
         b.first_frame = first + f0;
         const dim3 g((unsigned)((n + 255) / 256));
-        {
+        {   // path state + bounce-0 sampling
             ProfScope ps(c, PNRT_K_GEN);
-            hipLaunchKernelGGL(pt_wf_gen, g, dim3(256), 0, c->stream, fp, b, (const float4*)c->primary, c->colors);
+            hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, c->stream, s, fp, b, (const float4*)c->primary,
+                               c->colors);
         }
         HIPCHK(c, hipGetLastError());
         for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
             // segment dequeue counter (+ the WF_STATS census)
-            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 4, c->stream));
-            {
-                ProfScope ps(c, PNRT_K_SETUP);
-                hipLaunchKernelGGL(pt_wf_setup, g, dim3(256), 0, c->stream, s, fp, b);
-            }
+            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 32, c->stream));
             {
                 ProfScope ps(c, PNRT_K_TRACE);
                 if (c->debug_simple_trace)
@@ -248,6 +251,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
                     hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
                 else
                     hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+                if (WF_WIDE && !c->debug_simple_trace)   // non-finite rays: BVH2 pass (usually none)
+                    hipLaunchKernelGGL(pt_wf_trace_deferred, dim3(256), dim3(256), 0, c->stream, s, b, fp.mode);
             }
             HIPCHK(c, hipGetLastError());
             if (WF_STATS) {
@@ -286,7 +291,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
             }
             {
                 ProfScope ps(c, PNRT_K_SHADE);
-                hipLaunchKernelGGL(pt_wf_shade, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
+                // MIS + continuation, then the next bounce's sampling
+                hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
             }
             HIPCHK(c, hipGetLastError());
         }
@@ -468,6 +474,60 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     }
     uint32_t root_ref = childref(0);
     if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
+    // 4-wide collapse (DESIGN.md "Wide nodes"): wide node of BVH2 interior node k
+    // = slots (k.left.left, k.left.right, k.right.left, k.right.right), a leaf
+    // child taking one slot with its own box; pre-order, children allocated as met.
+    std::vector<float4> wnodes;
+    int wdepth = 0;
+    if (WF_WIDE && !(root_ref & REF_LEAF)) {
+        struct Item { uint32_t k, w; int depth; };
+        std::vector<Item> work{{root_ref, 0u, 0}};
+        wnodes.resize(8);
+        while (!work.empty()) {
+            Item it = work.back();
+            work.pop_back();
+            wdepth = it.depth > wdepth ? it.depth : wdepth;
+            const float* nk = reinterpret_cast<const float*>(&nodes[4 * (size_t)it.k]);
+            const uint32_t* mk = reinterpret_cast<const uint32_t*>(&nodes[4 * (size_t)it.k + 3]);
+            float box[4][6];
+            uint32_t ref[4];
+            uint32_t axes = mk[2] & 3u;
+            for (int side = 0; side < 2; ++side) {
+                const uint32_t cref = mk[side];
+                const float* cb = nk + 6 * side;                 // child box stored in the parent
+                if (cref & REF_LEAF) {
+                    for (int q = 0; q < 6; ++q) { box[2 * side][q] = cb[q]; box[2 * side + 1][q] = 0.f; }
+                    ref[2 * side] = cref;
+                    ref[2 * side + 1] = REF_NONE;
+                } else {
+                    const float* nc = reinterpret_cast<const float*>(&nodes[4 * (size_t)cref]);
+                    const uint32_t* mc = reinterpret_cast<const uint32_t*>(&nodes[4 * (size_t)cref + 3]);
+                    for (int g = 0; g < 2; ++g) {
+                        for (int q = 0; q < 6; ++q) box[2 * side + g][q] = nc[6 * g + q];
+                        ref[2 * side + g] = mc[g];
+                    }
+                    axes |= (mc[2] & 3u) << (2 + 2 * side);
+                }
+            }
+            for (int j = 3; j >= 0; --j)                         // allocate interior slots
+                if (!(ref[j] & REF_LEAF) && ref[j] != REF_NONE) {
+                    const uint32_t w = (uint32_t)(wnodes.size() / 8);
+                    wnodes.resize(wnodes.size() + 8);
+                    work.push_back({ref[j], w, it.depth + 1});
+                    ref[j] = w;
+                }
+            float4* o = &wnodes[8 * (size_t)it.w];
+            for (int q = 0; q < 6; ++q) o[q] = make_float4(box[0][q], box[1][q], box[2][q], box[3][q]);
+            uint32_t r4[4] = {ref[0], ref[1], ref[2], ref[3]}, m4[4] = {axes, 0u, 0u, 0u};
+            std::memcpy(&o[6], r4, 16);
+            std::memcpy(&o[7], m4, 16);
+        }
+    } else {
+        wnodes.resize(8);
+    }
+    // trace-kernel stack bound: one deferred sibling per BVH2 level, at most
+    // three per wide level
+    c->wf_stack_need = WF_WIDE ? 3 * (wdepth + 1) + 1 : maxd + 2;
     std::vector<float2> lights(nl);
     for (int i = 0; i < nl; ++i) {
         lights[i] = make_float2(Lt[3 * (size_t)i], Lt[3 * (size_t)i + 1]);
@@ -478,7 +538,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
 
     DevScene& s = c->scene;
     int rc;
-    if ((rc = upload(c, nodes, &s.nodes)) || (rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tris, &s.tris)) || (rc = upload(c, tidx, &s.tri_idx)) ||
+    if ((rc = upload(c, nodes, &s.nodes)) || (rc = upload(c, wnodes, &s.wnodes)) || (rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tris, &s.tris)) || (rc = upload(c, tidx, &s.tri_idx)) ||
         (rc = upload(c, verts, &s.verts)) || (rc = upload(c, mats, &s.materials)) || (rc = upload(c, lights, &s.lights)))
         return rc;
     s.n_nodes = (int)order.size(); s.n_tris = nt; s.n_verts = nv; s.n_materials = nm; s.n_lights = nl;
@@ -486,6 +546,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     const float* root = N;
     for (int k = 0; k < 3; ++k) { s.root_min[k] = root[k]; s.root_max[k] = root[3 + k]; }
     s.root_ref = root_ref;
+    s.wroot_ref = (root_ref & REF_LEAF) ? root_ref : 0u;
     c->root_is_leaf = fint(root[7]) == -1;
     c->n_interior = (int)order.size();
     c->max_depth = maxd;

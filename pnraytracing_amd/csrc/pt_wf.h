@@ -33,7 +33,6 @@ struct WfBufs {
     float4* S1;   // N.xyz, v
     float4* S2;   // Lo.xyz, bits(mat | (tex+1)<<24)
     float4* S3;   // cw.xyz, bits(seed)
-    float4* S4;   // V.xyz, bits(sample id: lr*W + x | slot << 28... see wf_id)
     float4* S5;   // base.xyz, -
     uint32_t* flags;
     // bounce candidates
@@ -46,7 +45,10 @@ struct WfBufs {
     // trace results
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
-    uint2* ovf;        // traversal stack spill
+    uint2* ovf;        // traversal stack spill, ovf_stride entries per trace lane
+    uint32_t ovf_stride;
+    uint32_t* defq;          // [3 * npad] rays the wide traversal hands to the BVH2 pass
+    unsigned int* defcount;
     unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
     // ray queues, written by setup without atomics: setup block j compacts its
     // paths' rays of kind k into segment (k, j) = rayq[k * npad + 256 j ...]
@@ -79,47 +81,26 @@ PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr,
     colors[((size_t)k * fp.rows + lr) * fp.width + x] = make_float4(color.x, color.y, color.z, 0.f);
 }
 
-// ---- gen: start every path from its pixel's primary hit --------------------------------------
-__global__ void __launch_bounds__(256) pt_wf_gen(FrameParams fp, WfBufs b, const float4* primary, float4* colors) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
-    int x, lr, k;
-    wf_coords(b, i, x, lr, k);
-    if (x >= fp.width || lr >= fp.rows) { b.flags[i] = 0; return; }
-    const float4* rec = primary + 3 * ((size_t)lr * fp.width + x);
-    float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
-    int mt = __float_as_int(q0.w);
-    f3 base = mk3(q2.y, q2.z, q2.w);
-    if (mt == -1) { b.flags[i] = 0; wf_write_color(fp, colors, k, lr, x, base); return; }   // primary miss
-    if (fp.max_depth == 0) { b.flags[i] = 0; wf_write_color(fp, colors, k, lr, x, add(base, mk3(0.f, 0.f, 0.f))); return; }
-    int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
-    uint32_t frame = b.first_frame + (uint32_t)k;
-    uint32_t seed = ((uint32_t)x * 1973u + (uint32_t)py * 9277u + frame * 26699u) | 1u;
-    f3 V = neg(camera_dir(fp, x, py));
-    b.S0[i] = make_float4(q0.x, q0.y, q0.z, q1.w);
-    b.S1[i] = make_float4(q1.x, q1.y, q1.z, q2.x);
-    b.S2[i] = make_float4(0.f, 0.f, 0.f, q0.w);
-    b.S3[i] = make_float4(1.f, 1.f, 1.f, __uint_as_float(seed));
-    b.S4[i] = make_float4(V.x, V.y, V.z, 0.f);
-    b.S5[i] = make_float4(base.x, base.y, base.z, 0.f);
-    b.flags[i] = WF_ALIVE;
-}
+// Path state a bounce's setup starts from (in registers: the fused kernels
+// hand it over without a round trip through HBM).
+struct PathIn {
+    f3 P, N, V, cw;
+    float u, v;
+    int mt;            // material | (texture + 1) << 24
+    uint32_t seed;
+};
 
 // ---- setup: one bounce's sampling and BRDF values (ray_tracing.comp:866-934) -----------------
-PN_DEV uint32_t wf_setup_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t fl) {
-    const int bounce = (int)((fl >> 8) & 7u);
-    int x, lr, k;
-    wf_coords(b, i, x, lr, k);
-    const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
-    const uint32_t frame = b.first_frame + (uint32_t)k;
-    float4 s0 = b.S0[i], s1 = b.S1[i], s2 = b.S2[i], s3 = b.S3[i], s4 = b.S4[i];
-    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z), V = mk3(s4.x, s4.y, s4.z);
-    int mt = __float_as_int(s2.w);
-    int hmat = mt & 0x00ffffff, htex = (int)((uint32_t)mt >> 24) - 1;
-    uint32_t seed = __float_as_uint(s3.w);
+// Returns the path's flags for the bounce (alive, bounce, which rays exist);
+// writes the bounce candidates C0-C3, shadow directions R0/R1, S3 and flags.
+PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, int bounce,
+                              int x, int py, uint32_t frame, const PathIn& q) {
+    const f3 P = q.P, N = q.N, V = q.V;
+    const int hmat = q.mt & 0x00ffffff, htex = (int)((uint32_t)q.mt >> 24) - 1;
+    uint32_t seed = q.seed;
 
     Material m = get_material(s, hmat);
-    if (htex != -1) m.baseColor = sample_albedo(s, htex, s0.w, s1.w);
+    if (htex != -1) m.baseColor = sample_albedo(s, htex, q.u, q.v);
     f3 T, B;
     if (N.z > 0.9999995f) T = mk3(1.f, 0.f, 0.f);
     else T = normalize(cross(N, mk3(0.f, 0.f, 1.f)));
@@ -220,7 +201,7 @@ PN_DEV uint32_t wf_setup_path(const DevScene& s, const FrameParams& fp, const Wf
     b.C1[i] = make_float4(LE.x, LE.y, LE.z, pe);
     b.C2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, NdotL);
     b.C3[i] = make_float4(L.x, L.y, L.z, dPDF);
-    b.S3[i] = make_float4(s3.x, s3.y, s3.z, __uint_as_float(seed));
+    b.S3[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(seed));
     b.flags[i] = nfl | WF_RCONT;
     return nfl | WF_RCONT;
 }
@@ -252,20 +233,62 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl) {
             wcnt[threadIdx.x][0] + wcnt[threadIdx.x][1] + wcnt[threadIdx.x][2] + wcnt[threadIdx.x][3];
 }
 
-__global__ void __launch_bounds__(256) pt_wf_setup(DevScene s, FrameParams fp, WfBufs b) {
+// ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
+__global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
+                                                       float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t nfl = 0;
     if (i < b.n) {
-        const uint32_t fl = b.flags[i];
-        if (fl & WF_ALIVE) nfl = wf_setup_path(s, fp, b, i, fl);
+        int x, lr, k;
+        wf_coords(b, i, x, lr, k);
+        b.flags[i] = 0;
+        if (x < fp.width && lr < fp.rows) {
+            const float4* rec = primary + 3 * ((size_t)lr * fp.width + x);
+            const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+            const int mt = __float_as_int(q0.w);
+            const f3 base = mk3(q2.y, q2.z, q2.w);
+            if (mt == -1) {                                   // primary miss: env colour only
+                wf_write_color(fp, colors, k, lr, x, base);
+            } else if (fp.max_depth == 0) {
+                wf_write_color(fp, colors, k, lr, x, add(base, mk3(0.f, 0.f, 0.f)));
+            } else {
+                const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+                const uint32_t frame = b.first_frame + (uint32_t)k;
+                PathIn q;
+                q.P = mk3(q0.x, q0.y, q0.z); q.N = mk3(q1.x, q1.y, q1.z);
+                q.u = q1.w; q.v = q2.x; q.mt = mt;
+                q.V = neg(camera_dir(fp, x, py));
+                q.cw = mk3(1.f, 1.f, 1.f);
+                q.seed = ((uint32_t)x * 1973u + (uint32_t)py * 9277u + frame * 26699u) | 1u;
+                b.S0[i] = make_float4(q.P.x, q.P.y, q.P.z, q.u);
+                b.S1[i] = make_float4(q.N.x, q.N.y, q.N.z, q.v);
+                b.S2[i] = make_float4(0.f, 0.f, 0.f, __int_as_float(mt));
+                b.S5[i] = make_float4(base.x, base.y, base.z, 0.f);
+                nfl = wf_setup_core(s, fp, b, i, 0, x, py, frame, q);
+            }
+        }
     }
     wf_enqueue(b, i, nfl);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
+// Finite origin, direction and 1/direction: the condition under which a wide
+// node's slot test implies the skipped intermediate box test.
+PN_DEV bool ray_finite(const RayP& r) {
+    const float m = 3.402823466e38f;
+    return pnm_fabs(r.o.x) <= m && pnm_fabs(r.o.y) <= m && pnm_fabs(r.o.z) <= m &&
+           pnm_fabs(r.d.x) <= m && pnm_fabs(r.d.y) <= m && pnm_fabs(r.d.z) <= m &&
+           pnm_fabs(r.inv.x) <= m && pnm_fabs(r.inv.y) <= m && pnm_fabs(r.inv.z) <= m;
+}
+PN_DEV void wf_swap_if(bool c, bool& ha, uint32_t& ra, float& za, bool& hb, uint32_t& rb, float& zb) {
+    const bool h = c ? hb : ha;  hb = c ? ha : hb;  ha = h;
+    const uint32_t q = c ? rb : ra;  rb = c ? ra : rb;  ra = q;
+    const float z = c ? zb : za;  zb = c ? za : zb;  za = z;
+}
+
 // Per-lane spill area of the traversal stack (address formed only when used).
 PN_DEV uint2* wf_ovf(const WfBufs& b, int tl) {
-    return b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * WF_OVF;
+    return b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride;
 }
 // Number of set bits of m below this lane (v_mbcnt).
 PN_DEV uint32_t lanes_below(uint64_t m) {
@@ -313,6 +336,12 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #endif
 #ifndef WF_MERGE_POP
 #define WF_MERGE_POP 1 // a popped node is visited in the same step
+#endif
+#ifndef WF_WIDE
+// trace kernel walks the 4-wide collapse of the BVH.  Measured on C2: 30 %
+// fewer iterations but 1.7x the kernel time (9 loads and ~150 VALU per node
+// step, 5 waves/SIMD), so the 2-wide walk is the default.
+#define WF_WIDE 0
 #endif
 #ifndef WF_STATS
 #define WF_STATS 0     // diagnostic builds: count iterations / lane steps per trace launch
@@ -399,17 +428,24 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         const uint32_t kind = ckind;
                         const uint32_t p = b.rayq[myid];
                         wf_load_ray(b, kind, p, mode, nr, ntmax, nany);
-                        float zlo;
-                        uint32_t root = REF_NONE;
-                        int nlt = 0, nlc = 0;
-                        if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
-                                     s.root_max[2], zlo)) {
-                            root = s.root_ref;
-                            if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
+                        if (WF_WIDE && !ray_finite(nr)) {
+                            // the wide tree skips the intermediate box tests, which is
+                            // exact only for finite rays (DESIGN.md "Wide nodes"):
+                            // hand this ray to the BVH2 pass
+                            b.defq[atomicAdd(b.defcount, 1u)] = (kind << 30) | p;
+                        } else {
+                            float zlo;
+                            uint32_t root = REF_NONE;
+                            int nlt = 0, nlc = 0;
+                            if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                                         s.root_max[2], zlo)) {
+                                root = WF_WIDE ? s.wroot_ref : s.root_ref;
+                                if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
+                            }
+                            r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
+                            hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
+                            busy = 1;
                         }
-                        r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
-                        hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
-                        busy = 1;
                     }
                 }
             }
@@ -476,6 +512,41 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     }
                     // WF_MERGE_POP: a popped interior node is visited in the same step
                     if (cur != REF_NONE && (WF_MERGE_POP || !popped_this_step)) {
+#if WF_WIDE
+                        // wide node: 4 slot boxes (SoA), 4 refs, the axes of the BVH2 node
+                        // and of its two children; slots are ordered exactly as the
+                        // reference's depth-first visit (:447-457) would reach them
+                        const float4* wn = s.wnodes + 8 * (size_t)cur;
+                        const float4 bx0 = wn[0], by0 = wn[1], bz0 = wn[2], bx1 = wn[3], by1 = wn[4], bz1 = wn[5];
+                        const uint4 rf = *reinterpret_cast<const uint4*>(wn + 6);
+                        const uint32_t ax = *reinterpret_cast<const uint32_t*>(wn + 7);
+                        const float tmc = tMax * 1.000001f;
+                        float z0, z1, z2, z3;
+                        bool h0 = box_fast<ID>(r, bx0.x, by0.x, bz0.x, bx1.x, by1.x, bz1.x, z0) && rf.x != REF_NONE;
+                        bool h1 = box_fast<ID>(r, bx0.y, by0.y, bz0.y, bx1.y, by1.y, bz1.y, z1) && rf.y != REF_NONE;
+                        bool h2 = box_fast<ID>(r, bx0.z, by0.z, bz0.z, bx1.z, by1.z, bz1.z, z2) && rf.z != REF_NONE;
+                        bool h3 = box_fast<ID>(r, bx0.w, by0.w, bz0.w, bx1.w, by1.w, bz1.w, z3) && rf.w != REF_NONE;
+                        if (r.cull_ok()) {
+                            if (z0 > tmc && z0 > 1e-20f) h0 = false;
+                            if (z1 > tmc && z1 > 1e-20f) h1 = false;
+                            if (z2 > tmc && z2 > 1e-20f) h2 = false;
+                            if (z3 > tmc && z3 > 1e-20f) h3 = false;
+                        }
+                        uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+                        // near child first at each of the two levels (rightFirst = dir[axis] < 0)
+                        wf_swap_if(comp(r.d, (int)((ax >> 2) & 3u)) < 0, h0, r0, z0, h1, r1, z1);
+                        wf_swap_if(comp(r.d, (int)((ax >> 4) & 3u)) < 0, h2, r2, z2, h3, r3, z3);
+                        const bool rN = comp(r.d, (int)(ax & 3u)) < 0;
+                        wf_swap_if(rN, h0, r0, z0, h2, r2, z2);
+                        wf_swap_if(rN, h1, r1, z1, h3, r3, z3);
+                        // visit the first hit slot now, defer the later hits (pushed last-first)
+                        uint32_t go = h0 ? r0 : (h1 ? r1 : (h2 ? r2 : (h3 ? r3 : REF_NONE)));
+                        const int first = h0 ? 0 : (h1 ? 1 : (h2 ? 2 : 3));
+                        if (h3 && first < 3) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, r3, z3);
+                        if (h2 && first < 2) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, r2, z2);
+                        if (h1 && first < 1) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, r1, z1);
+                        if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
+#else
                         const float4* nd = s.nodes + 4 * (size_t)cur;
                         float4 a = nd[0], bb = nd[1], c = nd[2];
                         uint4 m = *reinterpret_cast<const uint4*>(nd + 3);
@@ -494,6 +565,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         if (hNear && hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
                         uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
                         if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
+#endif
                         cur = go;
                     }
                 }
@@ -520,11 +592,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 }
 
 // ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
-__global__ void __launch_bounds__(256) pt_wf_shade(DevScene s, FrameParams fp, WfBufs b, float4* colors) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
-    uint32_t fl = b.flags[i];
-    if (!(fl & WF_ALIVE)) return;
+PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, float4* colors, uint32_t i) {
+    const uint32_t fl = b.flags[i];
+    if (!(fl & WF_ALIVE)) return 0;
     int bounce = (int)((fl >> 8) & 7u);
     float4 c0 = b.C0[i], c1 = b.C1[i], c2 = b.C2[i], c3 = b.C3[i];
     float4 s2 = b.S2[i], s3 = b.S3[i];
@@ -549,7 +619,7 @@ __global__ void __launch_bounds__(256) pt_wf_shade(DevScene s, FrameParams fp, W
         float4 s5 = b.S5[i];
         wf_write_color(fp, colors, k, lr, x, add(mk3(s5.x, s5.y, s5.z), Lo));
         b.flags[i] = 0;
-        return;
+        return 0;
     }
     float4 s0 = b.S0[i], s1 = b.S1[i];
     f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
@@ -563,15 +633,46 @@ __global__ void __launch_bounds__(256) pt_wf_shade(DevScene s, FrameParams fp, W
         float4 s5 = b.S5[i];
         wf_write_color(fp, colors, k, lr, x, add(mk3(s5.x, s5.y, s5.z), Lo));
         b.flags[i] = 0;
-        return;
+        return 0;
     }
-    f3 V = neg(L);
+    // the next bounce starts here: its setup runs on the state in registers
+    const int mt = (h.mat & 0x00ffffff) | ((h.tex + 1) << 24);
     b.S0[i] = make_float4(h.P.x, h.P.y, h.P.z, h.u);
     b.S1[i] = make_float4(h.N.x, h.N.y, h.N.z, h.v);
-    b.S2[i] = make_float4(Lo.x, Lo.y, Lo.z, __int_as_float((h.mat & 0x00ffffff) | ((h.tex + 1) << 24)));
-    b.S3[i] = make_float4(cw.x, cw.y, cw.z, s3.w);
-    b.S4[i] = make_float4(V.x, V.y, V.z, 0.f);
-    b.flags[i] = WF_ALIVE | ((uint32_t)bounce << 8);
+    b.S2[i] = make_float4(Lo.x, Lo.y, Lo.z, __int_as_float(mt));
+    PathIn q;
+    q.P = h.P; q.N = h.N; q.u = h.u; q.v = h.v; q.mt = mt;
+    q.V = neg(L); q.cw = cw; q.seed = __float_as_uint(s3.w);
+    const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+    return wf_setup_core(s, fp, b, i, bounce, x, py, b.first_frame + (uint32_t)k, q);
+}
+
+// ---- shade + next-bounce setup: MIS, continuation hit (:936-972), then the next
+// bounce's sampling for the paths that continue ----------------------------------------------
+__global__ void __launch_bounds__(256) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b, float4* colors) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, colors, i) : 0u;
+    wf_enqueue(b, i, nfl);     // every lane of the wave reaches this point
+}
+
+// BVH2 pass for the rays the wide traversal deferred (non-finite rays): one
+// thread per ray, the primary pass's traverse<>.
+__global__ void __launch_bounds__(256) pt_wf_trace_deferred(DevScene s, WfBufs b, int mode) {
+    const uint32_t cnt = *b.defcount;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += gridDim.x * blockDim.x) {
+        const uint32_t rid = b.defq[q], kind = rid >> 30, p = rid & 0x3fffffffu;
+        RayP r;
+        float tmax;
+        bool any;
+        wf_load_ray(b, kind, p, mode, r, tmax, any);
+        int hitTri = -1;
+        if (kind == 2) {
+            traverse<false>(s, r, tmax, hitTri);
+            b.hit[p] = hitTri;
+        } else {
+            b.occ[2 * (size_t)p + kind] = traverse<true>(s, r, tmax, hitTri) ? 1 : 0;
+        }
+    }
 }
 
 // Debug/reference variant of pt_wf_trace: one thread per ray, the verified
