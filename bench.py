@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2", choices=["C2", "C4", "C5"])
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
     ap.add_argument("--mode", default="zcull", choices=["exact", "zcull"])
     ap.add_argument("--kernel", default="v3", choices=["v1", "v3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
@@ -104,7 +104,7 @@ def main():
     from pnraytracing_amd.dist import ShardedFrame
     from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer
 
-    builders = {"C2": scenes.bunny_c2, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
+    builders = {"C2": scenes.bunny_c2, "C3": scenes.marry_c3, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
     cfg = builders[args.config]()
     W, H, spp = cfg.width, cfg.height, cfg.spp
 
@@ -190,7 +190,7 @@ def main():
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (procedural bunny stand-in, reference 1k HDR)",
+            "data": "synthetic: procedural stand-in meshes (reference OBJs absent), reference HDR/texture assets",
             "config": {"workload": f"{cfg.name}: {cfg.description}", "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",

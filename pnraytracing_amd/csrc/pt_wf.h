@@ -15,7 +15,12 @@
 #include <type_traits>
 #include "pt_passes.h"
 
+#ifndef WF_STACK
 #define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
+#endif
+#ifndef WF_REFILL_PCT
+#define WF_REFILL_PCT 50    // refill a wave when at most this % of its lanes still trace
+#endif
 #define WF_OVF 56
 #define WF_TRACE_BLOCK 256
 #define WF_CHUNK 256u        // rays per dequeue
@@ -305,10 +310,18 @@ PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, flo
 template <int STK>
 PN_DEV uint2 wf_pop(const uint2* lds, const uint2* ovf, int lane, int& sp) {
     --sp;
-    // unconditional LDS read + a rare global read (keeps the common pop a ds_read,
-    // not a flat load that would wait on every outstanding memory operation)
-    uint2 e = lds[(sp < STK ? sp : STK - 1) * WF_TRACE_BLOCK + lane];
-    if (sp >= STK) e = ovf[sp - STK];
+    // the common case is a ds_read; the rare spill read is a buffer load, which the
+    // compiler cannot merge with the LDS read into one flat load (a flat load waits
+    // for every outstanding vector-memory operation, stores included)
+    uint2 e;
+    if (sp >= STK) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)ovf, (short)0, 0x7fffffff, 0x00020000);
+        e.x = __builtin_amdgcn_raw_buffer_load_b32(rs, (sp - STK) * 8, 0, 0);
+        e.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (sp - STK) * 8 + 4, 0, 0);
+    } else {
+        e = lds[sp * WF_TRACE_BLOCK + lane];
+    }
     return e;
 }
 
@@ -342,6 +355,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 // fewer iterations but 1.7x the kernel time (9 loads and ~150 VALU per node
 // step, 5 waves/SIMD), so the 2-wide walk is the default.
 #define WF_WIDE 0
+#endif
+#ifndef WF_DIAG_NOSTORE
+#define WF_DIAG_NOSTORE 0   // timing experiment: drop the trace results (wrong images)
 #endif
 #ifndef WF_STATS
 #define WF_STATS 0     // diagnostic builds: count iterations / lane steps per trace launch
@@ -457,7 +473,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (exhausted) break;
             continue;
         }
-        const int thr = SYNC ? 0 : __popcll(busym) / 2;
+        const int thr = SYNC ? 0 : (__popcll(busym) * WF_REFILL_PCT) / 100;
         // ---- traverse until half of the lanes have finished their ray ------------------
         // (IDENT: no lane of the wave needs the triangle test's axis permutation)
         auto run = [&](auto ident_tag) {
@@ -571,7 +587,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 }
                 if (done) {
                     const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
-                    if (WF_NT) {
+                    if (WF_DIAG_NOSTORE) {
+                        // timing experiment only: results are dropped
+                    } else if (WF_NT) {
                         if (kind == 2) __builtin_nontemporal_store(hitTri, b.hit + p);
                         else __builtin_nontemporal_store((uint8_t)(hitTri >= 0 ? 1 : 0), b.occ + 2 * (size_t)p + kind);
                     } else {

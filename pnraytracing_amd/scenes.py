@@ -94,6 +94,53 @@ def bunny_c2(width=1920, height=1080, spp=4, nu=264, nv=132, env=True) -> SceneC
                                    f"{width}x{height}, {spp} spp")
 
 
+def load_texture(path: str):
+    """stbi_load(path, &w, &h, &n, 0) as model.hpp:66-73 calls it: 8-bit rows
+    top-first, no vertical flip, the file's own channel count."""
+    from PIL import Image
+    im = Image.open(path)
+    if im.mode not in ("L", "RGB", "RGBA"):
+        im = im.convert("RGBA")
+    px = np.asarray(im, np.uint8)
+    ch = 1 if px.ndim == 2 else px.shape[2]
+    return (np.ascontiguousarray(px).reshape(-1), im.width, im.height, ch)
+
+
+def checker_texture(w: int, h: int, ch: int = 3, seed: int = 7):
+    """Deterministic 8-bit test texture (odd widths exercise GL_UNPACK_ALIGNMENT 4)."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = ((x // 8 + y // 8) % 2) * 160 + 40
+    px = np.stack([(base + rng.integers(0, 50, (h, w))) % 256 for _ in range(ch)], -1).astype(np.uint8)
+    return (px.reshape(-1), w, h, ch)
+
+
+def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144) -> SceneConfig:
+    """C3: CornellBox() with its commented-out "marry" model (main.cpp:209) -- a
+    UV-mapped ~50k-triangle figure stand-in textured with MC003_Kozakura_Mari.png
+    (RGBA 2048x1024, texture unit 5) -- plus SceneFlat()'s metal boards
+    (main.cpp:254-292, Disney metallic/roughness varied) carrying an RGB texture
+    of odd width, and the 1k env.  Every Disney lobe is non-zero somewhere."""
+    sb = H.SceneBuilder()
+    m = H.Material(baseColor=(0.65, 0.65, 0.65))
+    figure = H.mesh_displaced_sphere(nu, nv, 1.0, (0.0, 0.0, 0.0), 0.05, 0xA11CE)
+    fm = H.Material(baseColor=(0.8, 0.8, 0.8), subsurface=0.3, specular=0.5, specularTint=0.2, roughness=0.45,
+                    anisotropic=0.3, sheen=0.4, sheenTint=0.5, clearcoat=0.6, clearcoatGloss=0.8)
+    sb.add_model(figure, [H.translate(0.1, 1.55, -0.5), H.scale(0.75, 1.5, 0.6)], fm, "marry", texture_ids=[0])
+    _cornell_walls(sb, m)
+    board = H.mesh_quad(27.5)
+    for k, (met, rough, z) in enumerate([(0.95, 0.02, -2.2), (0.80, 0.15, -1.4), (0.60, 0.35, -0.6)]):
+        bm = H.Material(baseColor=(0.83, 0.83, 0.83), metallic=met, roughness=rough)
+        sb.add_model(board, [H.translate(-1.6 + 1.6 * k, 0.6, z), H.rotate(50.0 - 15.0 * k, 1, 0, 0),
+                             H.scale(0.012, 1.0, 0.004)], bm, f"board{k + 1}", texture_ids=[1])
+    rgb, tab = _env_1k()
+    tex = [load_texture(MARI_PNG), checker_texture(333, 97, 3)]
+    return SceneConfig("C3-marry", sb.build(), _cornell_camera(width, height), width, height, spp,
+                       env_rgb=rgb, env_table=tab, textures=tex,
+                       description=f"Cornell + textured figure stand-in ({nu * nv * 2} tris, Mari 2048x1024 RGBA) "
+                                   f"+ metal boards (RGB 333x97) + 1k env")
+
+
 def teapot_c4(width=1920, height=1080, spp=4) -> SceneConfig:
     """C4: teapot() scene (main.cpp:329-347) + an emissive quad and the 1k env,
     so the light, environment and BSDF pdfs are all active."""
@@ -125,4 +172,4 @@ def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, e
                        description=f"{nu * nv * 2}-tri displaced sphere + {env_w}x{env_h} synthetic env")
 
 
-CONFIGS = {"C1": cornell_c1, "C2": bunny_c2, "C4": teapot_c4, "C5": synthetic_c5}
+CONFIGS = {"C1": cornell_c1, "C2": bunny_c2, "C3": marry_c3, "C4": teapot_c4, "C5": synthetic_c5}

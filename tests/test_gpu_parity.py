@@ -131,6 +131,38 @@ def test_c4_rows_bitwise(pt):
     assert_bitwise(got[rows], ref[rows], "C4 rows")
 
 
+def test_c3_textured_bitwise(pt):
+    """Albedo textures: RGBA 2048x1024 (REPEAT, bilinear, UNORM8) and an RGB
+    texture of odd width (GL_UNPACK_ALIGNMENT 4 row skew); all Disney lobes."""
+    c = cfg("C3", width=192, height=108)
+    got = gpu_render(pt, c, 0, 4)
+    ref, st = pyoracle.Oracle(c).render(0, 4)
+    assert st["albedo_bytes"] > 0
+    assert_bitwise(got, ref, "C3 192x108")
+
+
+def test_c3_fullsize_rows_bitwise(pt):
+    c = cfg("C3")
+    got = gpu_render(pt, c, 4, 4)
+    ref = np.zeros_like(got)
+    pyoracle.Oracle(c).render(4, 4, rows=(3, c.height), y_step=45, accum=ref)
+    rows = np.arange(3, c.height, 45)
+    assert_bitwise(got[rows], ref[rows], "C3 1080p rows")
+
+
+def test_c5_4m_triangles_rows_bitwise(pt):
+    """4.19M-triangle BVH (depth, leaf-table refs, stack spill) + 4k synthetic
+    env, at a reduced resolution."""
+    c = cfg("C5", width=320, height=180)
+    got = gpu_render(pt, c, 0, 2)
+    info = pt.device_info()
+    assert info["n_triangles"] == c.n_triangles and info["n_interior"] > 1_000_000
+    ref = np.zeros_like(got)
+    pyoracle.Oracle(c).render(0, 2, rows=(1, c.height), y_step=6, accum=ref)
+    rows = np.arange(1, c.height, 6)
+    assert_bitwise(got[rows], ref[rows], "C5 rows")
+
+
 # ---- size-independent properties at full size ------------------------------------------------
 def test_traversal_modes_agree_fullsize(pt):
     """z-slab culling is result-neutral and both kernels compute the same
