@@ -189,7 +189,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
-    const size_t per_path = 16 * 11 + 4 + 4 + 2 + 24 + 1;  // S0-3,S5, C0-3, R0-1 | flags | hit | occ | ray + deferred queues | counts
+    const size_t per_path = 16 * 11 + 4 + 4 + 2 + 12 + 1;  // S0-3,S5, C0-3, R0-1 | flags | hit | occ | ray queues | counts
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
@@ -217,12 +217,10 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         b.npad = (uint32_t)((n + 255) / 256 * 256);
         b.nseg_k = b.npad / 256;
         b.rayq = reinterpret_cast<uint32_t*>(base + off); off += (size_t)b.npad * 12;
-        b.defq = reinterpret_cast<uint32_t*>(base + off); off += (size_t)b.npad * 12;
         b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
         off = (off + 255) & ~(size_t)255;
         off = (off + 255) & ~(size_t)255;
         b.counter = reinterpret_cast<unsigned int*>(base + off);
-        b.defcount = b.counter + 4;
         b.stats = reinterpret_cast<unsigned long long*>(base + off + 64); off += 256;
         b.ovf = c->wf_ovf;
         b.ovf_stride = (uint32_t)ovf_stride;
@@ -251,15 +249,13 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
                     hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
                 else
                     hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
-                if (WF_WIDE && !c->debug_simple_trace)   // non-finite rays: BVH2 pass (usually none)
-                    hipLaunchKernelGGL(pt_wf_trace_deferred, dim3(256), dim3(256), 0, c->stream, s, b, fp.mode);
             }
             HIPCHK(c, hipGetLastError());
             if (WF_STATS) {
                 unsigned long long st[8];
                 HIPCHK(c, hipStreamSynchronize(c->stream));
                 HIPCHK(c, hipMemcpy(st, b.stats, sizeof st, hipMemcpyDeviceToHost));
-                fprintf(stderr, "[trace stats] bounce %d n=%zu iters=%llu active/iter=%.1f tri=%llu pop=%llu node=%llu "
+                fprintf(stderr, "[trace stats] bounce %d n=%zu iters=%llu active/iter=%.1f tri=%llu node=%llu pop-only=%llu "
                         "refills=%llu rays=%llu  lane-steps/ray=%.1f\n", bounce, n, st[0], st[0] ? (double)st[1] / st[0] : 0.0,
                         st[2], st[3], st[4], st[5], st[6], st[6] ? (double)st[1] / st[6] : 0.0);
             }
@@ -391,7 +387,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     c->scene_bytes = 0;
 
     // triangles: positions gathered in BVH order, ids validated
-    std::vector<float4> tris((size_t)nt * 3);
+    std::vector<float4> tris((size_t)nt * 3 + 1);   // +1: the trace kernel reads 64 B per record
     std::vector<int4> tidx(nt);
     for (int i = 0; i < nt; ++i) {
         const float* t = T + 6 * (size_t)i;
@@ -446,6 +442,19 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     }
     if (maxd >= PT_STACK - 1)
         return set_err(c, PNRT_E_SCENE, "BVH depth " + std::to_string(maxd) + " exceeds the kernel stack");
+    // device numbering: breadth-first, so the top levels are the first indices
+    // (the trace kernel keeps nodes [0, WF_TREELET) in LDS); the visit order is
+    // carried by the child refs and the axis, not by the numbering
+    order.clear();
+    if (fint(N[7]) != -1) order.push_back(0);
+    for (size_t q = 0; q < order.size(); ++q) {
+        const int i = order[q];
+        dn[i] = (int)q;
+        const float* n = N + 12 * (size_t)i;
+        const int rc = fint(n[7]);
+        if (fint(N[12 * (size_t)(i + 1) + 7]) != -1) order.push_back(i + 1);
+        if (fint(N[12 * (size_t)rc + 7]) != -1) order.push_back(rc);
+    }
     // packed child reference (pt_common.h): interior -> node index, leaf -> range
     std::vector<int2> leaf_table;
     auto childref = [&](int ci) -> uint32_t {
@@ -457,7 +466,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         leaf_table.push_back(make_int2(s0, cnt));
         return REF_LEAF | REF_TABLE | (uint32_t)(leaf_table.size() - 1);
     };
-    if ((int64_t)order.size() >= (1 << 30)) return set_err(c, PNRT_E_SCENE, "too many BVH nodes");
+    if ((int64_t)order.size() >= (1 << 25)) return set_err(c, PNRT_E_SCENE, "too many BVH nodes (2 GB node buffer limit)");
     if (nm >= (1 << 24)) return set_err(c, PNRT_E_SCENE, "too many materials");
     std::vector<float4> nodes(order.size() * 4);
     for (size_t k = 0; k < order.size(); ++k) {
@@ -474,60 +483,8 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     }
     uint32_t root_ref = childref(0);
     if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
-    // 4-wide collapse (DESIGN.md "Wide nodes"): wide node of BVH2 interior node k
-    // = slots (k.left.left, k.left.right, k.right.left, k.right.right), a leaf
-    // child taking one slot with its own box; pre-order, children allocated as met.
-    std::vector<float4> wnodes;
-    int wdepth = 0;
-    if (WF_WIDE && !(root_ref & REF_LEAF)) {
-        struct Item { uint32_t k, w; int depth; };
-        std::vector<Item> work{{root_ref, 0u, 0}};
-        wnodes.resize(8);
-        while (!work.empty()) {
-            Item it = work.back();
-            work.pop_back();
-            wdepth = it.depth > wdepth ? it.depth : wdepth;
-            const float* nk = reinterpret_cast<const float*>(&nodes[4 * (size_t)it.k]);
-            const uint32_t* mk = reinterpret_cast<const uint32_t*>(&nodes[4 * (size_t)it.k + 3]);
-            float box[4][6];
-            uint32_t ref[4];
-            uint32_t axes = mk[2] & 3u;
-            for (int side = 0; side < 2; ++side) {
-                const uint32_t cref = mk[side];
-                const float* cb = nk + 6 * side;                 // child box stored in the parent
-                if (cref & REF_LEAF) {
-                    for (int q = 0; q < 6; ++q) { box[2 * side][q] = cb[q]; box[2 * side + 1][q] = 0.f; }
-                    ref[2 * side] = cref;
-                    ref[2 * side + 1] = REF_NONE;
-                } else {
-                    const float* nc = reinterpret_cast<const float*>(&nodes[4 * (size_t)cref]);
-                    const uint32_t* mc = reinterpret_cast<const uint32_t*>(&nodes[4 * (size_t)cref + 3]);
-                    for (int g = 0; g < 2; ++g) {
-                        for (int q = 0; q < 6; ++q) box[2 * side + g][q] = nc[6 * g + q];
-                        ref[2 * side + g] = mc[g];
-                    }
-                    axes |= (mc[2] & 3u) << (2 + 2 * side);
-                }
-            }
-            for (int j = 3; j >= 0; --j)                         // allocate interior slots
-                if (!(ref[j] & REF_LEAF) && ref[j] != REF_NONE) {
-                    const uint32_t w = (uint32_t)(wnodes.size() / 8);
-                    wnodes.resize(wnodes.size() + 8);
-                    work.push_back({ref[j], w, it.depth + 1});
-                    ref[j] = w;
-                }
-            float4* o = &wnodes[8 * (size_t)it.w];
-            for (int q = 0; q < 6; ++q) o[q] = make_float4(box[0][q], box[1][q], box[2][q], box[3][q]);
-            uint32_t r4[4] = {ref[0], ref[1], ref[2], ref[3]}, m4[4] = {axes, 0u, 0u, 0u};
-            std::memcpy(&o[6], r4, 16);
-            std::memcpy(&o[7], m4, 16);
-        }
-    } else {
-        wnodes.resize(8);
-    }
-    // trace-kernel stack bound: one deferred sibling per BVH2 level, at most
-    // three per wide level
-    c->wf_stack_need = WF_WIDE ? 3 * (wdepth + 1) + 1 : maxd + 2;
+    // trace-kernel stack bound: at most one deferred sibling per BVH level
+    c->wf_stack_need = maxd + 2;
     std::vector<float2> lights(nl);
     for (int i = 0; i < nl; ++i) {
         lights[i] = make_float2(Lt[3 * (size_t)i], Lt[3 * (size_t)i + 1]);
@@ -538,7 +495,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
 
     DevScene& s = c->scene;
     int rc;
-    if ((rc = upload(c, nodes, &s.nodes)) || (rc = upload(c, wnodes, &s.wnodes)) || (rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tris, &s.tris)) || (rc = upload(c, tidx, &s.tri_idx)) ||
+    if ((rc = upload(c, nodes, &s.nodes)) || (rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tris, &s.tris)) || (rc = upload(c, tidx, &s.tri_idx)) ||
         (rc = upload(c, verts, &s.verts)) || (rc = upload(c, mats, &s.materials)) || (rc = upload(c, lights, &s.lights)))
         return rc;
     s.n_nodes = (int)order.size(); s.n_tris = nt; s.n_verts = nv; s.n_materials = nm; s.n_lights = nl;
@@ -546,7 +503,6 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     const float* root = N;
     for (int k = 0; k < 3; ++k) { s.root_min[k] = root[k]; s.root_max[k] = root[3 + k]; }
     s.root_ref = root_ref;
-    s.wroot_ref = (root_ref & REF_LEAF) ? root_ref : 0u;
     c->root_is_leaf = fint(root[7]) == -1;
     c->n_interior = (int)order.size();
     c->max_depth = maxd;

@@ -48,10 +48,6 @@ struct DevScene {
     float lights_sum_area;
     float root_min[3], root_max[3];
     uint32_t root_ref;
-    // 4-wide collapse of the same tree for the wavefront trace kernel (pt_wf.h):
-    // wide node = the grandchildren of a BVH2 interior node, 8 float4 each
-    const float4* wnodes;
-    uint32_t wroot_ref;         // wide index 0, or the root's leaf ref
     int has_hdr, hdr_w, hdr_h;
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad

@@ -52,8 +52,6 @@ struct WfBufs {
     int* hit;          // continuation hit triangle or -1
     uint2* ovf;        // traversal stack spill, ovf_stride entries per trace lane
     uint32_t ovf_stride;
-    uint32_t* defq;          // [3 * npad] rays the wide traversal hands to the BVH2 pass
-    unsigned int* defcount;
     unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
     // ray queues, written by setup without atomics: setup block j compacts its
     // paths' rays of kind k into segment (k, j) = rayq[k * npad + 256 j ...]
@@ -277,20 +275,6 @@ __global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams f
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
-// Finite origin, direction and 1/direction: the condition under which a wide
-// node's slot test implies the skipped intermediate box test.
-PN_DEV bool ray_finite(const RayP& r) {
-    const float m = 3.402823466e38f;
-    return pnm_fabs(r.o.x) <= m && pnm_fabs(r.o.y) <= m && pnm_fabs(r.o.z) <= m &&
-           pnm_fabs(r.d.x) <= m && pnm_fabs(r.d.y) <= m && pnm_fabs(r.d.z) <= m &&
-           pnm_fabs(r.inv.x) <= m && pnm_fabs(r.inv.y) <= m && pnm_fabs(r.inv.z) <= m;
-}
-PN_DEV void wf_swap_if(bool c, bool& ha, uint32_t& ra, float& za, bool& hb, uint32_t& rb, float& zb) {
-    const bool h = c ? hb : ha;  hb = c ? ha : hb;  ha = h;
-    const uint32_t q = c ? rb : ra;  rb = c ? ra : rb;  ra = q;
-    const float z = c ? zb : za;  zb = c ? za : zb;  za = z;
-}
-
 // Per-lane spill area of the traversal stack (address formed only when used).
 PN_DEV uint2* wf_ovf(const WfBufs& b, int tl) {
     return b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride;
@@ -328,6 +312,7 @@ PN_DEV uint2 wf_pop(const uint2* lds, const uint2* ovf, int lane, int& sp) {
 // BoundIntersect (:213-228) for traversal decisions.  fminf/fmaxf (v_min/v_max)
 // drop NaNs exactly like the oracle's min/max; the results only feed
 // comparisons, where the sign of a zero cannot matter -> same booleans.
+// Returns the box's z-slab lower end (zlo) in the triangle test's frame.
 template <bool IDENT = false>
 PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
                      float& zlo) {
@@ -344,58 +329,40 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return (t1 >= t0) && !(r.cull_ok() && hi <= 0.0f);
 }
 
-#ifndef WF_TRI2
-#define WF_TRI2 0      // two triangle tests per traversal step
-#endif
-#ifndef WF_MERGE_POP
-#define WF_MERGE_POP 1 // a popped node is visited in the same step
-#endif
-#ifndef WF_WIDE
-// trace kernel walks the 4-wide collapse of the BVH.  Measured on C2: 30 %
-// fewer iterations but 1.7x the kernel time (9 loads and ~150 VALU per node
-// step, 5 waves/SIMD), so the 2-wide walk is the default.
-#define WF_WIDE 0
-#endif
 #ifndef WF_DIAG_NOSTORE
 #define WF_DIAG_NOSTORE 0   // timing experiment: drop the trace results (wrong images)
 #endif
 #ifndef WF_STATS
-#define WF_STATS 0     // diagnostic builds: count iterations / lane steps per trace launch
+#define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
-#ifndef WF_NT
-#define WF_NT 0        // non-temporal path-state traffic in the trace kernel (keeps the BVH in L2)
-#endif
-template <typename T>
-PN_DEV T wf_ld(const T* a) {
-    if (WF_NT) return __builtin_nontemporal_load(a);
-    return *a;
-}
-PN_DEV float4 wf_ld4(const float4* a) {
-    if (WF_NT) {
-        const float* f = reinterpret_cast<const float*>(a);
-        return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1),
-                           __builtin_nontemporal_load(f + 2), __builtin_nontemporal_load(f + 3));
-    }
-    return *a;
-}
 
 // Load ray (kind, path p) of the bounce into a lane.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t p, int mode, RayP& r, float& tmax, bool& any) {
-    float4 s0 = wf_ld4(b.S0 + p), s1 = wf_ld4(b.S1 + p);
+    float4 s0 = b.S0[p], s1 = b.S1[p];
     f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
-    float4 dv = wf_ld4(kind == 0 ? b.R0 + p : (kind == 1 ? b.R1 + p : b.C3 + p));
+    float4 dv = kind == 0 ? b.R0[p] : (kind == 1 ? b.R1[p] : b.C3[p]);
     f3 o = kind == 1 ? P : add(P, muls(N, 0.0001f));
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
     r = make_ray(o, mk3(dv.x, dv.y, dv.z), mode);
 }
 
-// Persistent traversal of every ray of the bounce.  Control flow is kept
-// structured and loop-free inside a lane's step (one triangle test, one node,
-// or one stack pop per iteration) with every wave-level decision (ballot) at a
-// reconvergence point: the ray <-> lane refill runs once per outer iteration.
+// Persistent traversal of every queued ray of the bounce.
+//
+// One "step" per lane and loop iteration, with a single memory fetch issued by
+// the same instructions for every lane: a lane that has a triangle pending
+// loads its 48-B record (tris are padded so the 64-B read is in bounds), a lane
+// at an interior node loads the node's 64 B (both child boxes, refs, axis).
+// The step then runs the triangle test or the node visit, and finally resolves
+// the lane's next fetch target -- popping the LDS stack (z-culled entries are
+// dropped) -- so a wave with lanes in both states waits for ONE memory latency
+// per iteration, not two.  Per lane the sequence of triangle tests and node
+// visits is exactly the reference's (near child first, :447-457).
+// Control flow stays structured and loop-free inside a step with every
+// wave-level decision (ballot) at a reconvergence point: the ray <-> lane
+// refill runs between traversal phases.
 #ifndef WF_TRACE_WAVES
-#define WF_TRACE_WAVES 1      // minimum waves per SIMD requested from the register allocator
+#define WF_TRACE_WAVES 5      // waves per SIMD requested from the register allocator (98 -> 96 VGPRs)
 #endif
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
@@ -413,7 +380,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     uint32_t cur = REF_NONE, rid = 0;
     bool any = true;
     int busy = 0;
-    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, pop, node, refill, rays, -
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
 
     for (;;) {
         // ---- refill: idle lanes take the wave's next queued rays; more passes when a
@@ -437,32 +404,22 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 const uint32_t myid = next + lanes_below(idle);
                 next = min(next + (uint32_t)__popcll(idle), end);
                 if (busy == 0 && myid < end) {
+                    const uint32_t kind = ckind, p = b.rayq[myid];
                     RayP nr;
                     float ntmax;
                     bool nany;
-                    {
-                        const uint32_t kind = ckind;
-                        const uint32_t p = b.rayq[myid];
-                        wf_load_ray(b, kind, p, mode, nr, ntmax, nany);
-                        if (WF_WIDE && !ray_finite(nr)) {
-                            // the wide tree skips the intermediate box tests, which is
-                            // exact only for finite rays (DESIGN.md "Wide nodes"):
-                            // hand this ray to the BVH2 pass
-                            b.defq[atomicAdd(b.defcount, 1u)] = (kind << 30) | p;
-                        } else {
-                            float zlo;
-                            uint32_t root = REF_NONE;
-                            int nlt = 0, nlc = 0;
-                            if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
-                                         s.root_max[2], zlo)) {
-                                root = WF_WIDE ? s.wroot_ref : s.root_ref;
-                                if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
-                            }
-                            r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
-                            hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
-                            busy = 1;
-                        }
+                    wf_load_ray(b, kind, p, mode, nr, ntmax, nany);
+                    float zlo;
+                    uint32_t root = REF_NONE;
+                    int nlt = 0, nlc = 0;
+                    if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                                 s.root_max[2], zlo)) {
+                        root = s.root_ref;
+                        if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
+                    r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
+                    hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
+                    busy = 1;
                 }
             }
         };
@@ -474,46 +431,57 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             continue;
         }
         const int thr = SYNC ? 0 : (__popcll(busym) * WF_REFILL_PCT) / 100;
-        // ---- traverse until half of the lanes have finished their ray ------------------
+        // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------
         // (IDENT: no lane of the wave needs the triangle test's axis permutation)
         auto run = [&](auto ident_tag) {
-        constexpr bool ID = decltype(ident_tag)::value;
-        for (;;) {
-            if (WF_STATS) {
-                st[0] += 1;
-                st[1] += __popcll(__ballot(busy != 0));
-                st[2] += __popcll(__ballot(busy != 0 && lc > 0));
-                st[3] += __popcll(__ballot(busy != 0 && lc <= 0 && cur == REF_NONE && sp > 0));
-                st[4] += __popcll(__ballot(busy != 0 && lc <= 0 && (cur != REF_NONE || (WF_MERGE_POP && sp > 0))));
-            }
-            if (busy) {
-                bool done = false;
-                bool popped_this_step = cur == REF_NONE;
-                if (lc > 0) {
-                    // one triangle per step, or two (WF_TRI2): both records are
-                    // loaded up front, tested in BVH order (the second sees the
-                    // tMax the first may have set; any-hit stops at the first)
-                    const float4* tp = s.tris + 3 * (size_t)lt;
-                    const bool two = WF_TRI2 && lc >= 2;
-                    float4 q0 = tp[0], q1 = tp[1], q2 = tp[2], q3, q4, q5;
-                    if (two) { q3 = tp[3]; q4 = tp[4]; q5 = tp[5]; }
-                    float e0, e1, e2, det, ts;
-                    if (tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts)) {
-                        hitTri = lt;
-                        if (any) done = true;
-                        else tMax = ts * (1.0f / det);
+            constexpr bool ID = decltype(ident_tag)::value;
+            for (;;) {
+                if (WF_STATS) {
+                    st[0] += 1;
+                    st[1] += __popcll(__ballot(busy != 0));
+                    st[2] += __popcll(__ballot(busy != 0 && lc > 0));
+                    st[3] += __popcll(__ballot(busy != 0 && lc <= 0 && cur != REF_NONE));
+                    st[4] += __popcll(__ballot(busy != 0 && lc <= 0 && cur == REF_NONE));
+                }
+                if (busy) {
+                    bool done = false;
+                    const bool isTri = lc > 0;
+                    // ---- the step's single fetch: a triangle record or a node
+                    float4 q0, q1, q2, q3;
+                    if (isTri || cur != REF_NONE) {
+                        const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)cur;
+                        q0 = base[0]; q1 = base[1]; q2 = base[2]; q3 = base[3];
                     }
-                    ++lt; --lc;
-                    if (two && !done) {
-                        if (tri_test<ID>(r, q3, q4, q5, tMax, e0, e1, e2, det, ts)) {
+                    if (isTri) {
+                        float e0, e1, e2, det, ts;
+                        if (tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts)) {
                             hitTri = lt;
                             if (any) done = true;
                             else tMax = ts * (1.0f / det);
                         }
                         ++lt; --lc;
+                    } else if (cur != REF_NONE) {
+                        const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y),
+                                                   __float_as_uint(q3.z), __float_as_uint(q3.w));
+                        const float tmc = tMax * 1.000001f;
+                        float zloL, zloR;
+                        bool hL = box_fast<ID>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+                        bool hR = box_fast<ID>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
+                        if (r.cull_ok()) {
+                            if (zloL > tmc && zloL > 1e-20f) hL = false;
+                            if (zloR > tmc && zloR > 1e-20f) hR = false;
+                        }
+                        bool rightFirst = comp(r.d, (int)m.z) < 0;     // :448
+                        uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+                        bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+                        float zFar = rightFirst ? zloL : zloR;
+                        if (hNear && hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
+                        uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
+                        if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
+                        cur = go;
                     }
-                } else {
-                    if (cur == REF_NONE) {
+                    // ---- next fetch target: pop when nothing is pending
+                    if (!done && lc <= 0 && cur == REF_NONE) {
                         if (sp == 0) {
                             done = true;
                         } else {
@@ -526,81 +494,17 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                             }
                         }
                     }
-                    // WF_MERGE_POP: a popped interior node is visited in the same step
-                    if (cur != REF_NONE && (WF_MERGE_POP || !popped_this_step)) {
-#if WF_WIDE
-                        // wide node: 4 slot boxes (SoA), 4 refs, the axes of the BVH2 node
-                        // and of its two children; slots are ordered exactly as the
-                        // reference's depth-first visit (:447-457) would reach them
-                        const float4* wn = s.wnodes + 8 * (size_t)cur;
-                        const float4 bx0 = wn[0], by0 = wn[1], bz0 = wn[2], bx1 = wn[3], by1 = wn[4], bz1 = wn[5];
-                        const uint4 rf = *reinterpret_cast<const uint4*>(wn + 6);
-                        const uint32_t ax = *reinterpret_cast<const uint32_t*>(wn + 7);
-                        const float tmc = tMax * 1.000001f;
-                        float z0, z1, z2, z3;
-                        bool h0 = box_fast<ID>(r, bx0.x, by0.x, bz0.x, bx1.x, by1.x, bz1.x, z0) && rf.x != REF_NONE;
-                        bool h1 = box_fast<ID>(r, bx0.y, by0.y, bz0.y, bx1.y, by1.y, bz1.y, z1) && rf.y != REF_NONE;
-                        bool h2 = box_fast<ID>(r, bx0.z, by0.z, bz0.z, bx1.z, by1.z, bz1.z, z2) && rf.z != REF_NONE;
-                        bool h3 = box_fast<ID>(r, bx0.w, by0.w, bz0.w, bx1.w, by1.w, bz1.w, z3) && rf.w != REF_NONE;
-                        if (r.cull_ok()) {
-                            if (z0 > tmc && z0 > 1e-20f) h0 = false;
-                            if (z1 > tmc && z1 > 1e-20f) h1 = false;
-                            if (z2 > tmc && z2 > 1e-20f) h2 = false;
-                            if (z3 > tmc && z3 > 1e-20f) h3 = false;
+                    if (done) {
+                        const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
+                        if (!WF_DIAG_NOSTORE) {
+                            if (kind == 2) b.hit[p] = hitTri;
+                            else b.occ[2 * (size_t)p + kind] = hitTri >= 0 ? 1 : 0;
                         }
-                        uint32_t r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-                        // near child first at each of the two levels (rightFirst = dir[axis] < 0)
-                        wf_swap_if(comp(r.d, (int)((ax >> 2) & 3u)) < 0, h0, r0, z0, h1, r1, z1);
-                        wf_swap_if(comp(r.d, (int)((ax >> 4) & 3u)) < 0, h2, r2, z2, h3, r3, z3);
-                        const bool rN = comp(r.d, (int)(ax & 3u)) < 0;
-                        wf_swap_if(rN, h0, r0, z0, h2, r2, z2);
-                        wf_swap_if(rN, h1, r1, z1, h3, r3, z3);
-                        // visit the first hit slot now, defer the later hits (pushed last-first)
-                        uint32_t go = h0 ? r0 : (h1 ? r1 : (h2 ? r2 : (h3 ? r3 : REF_NONE)));
-                        const int first = h0 ? 0 : (h1 ? 1 : (h2 ? 2 : 3));
-                        if (h3 && first < 3) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, r3, z3);
-                        if (h2 && first < 2) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, r2, z2);
-                        if (h1 && first < 1) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, r1, z1);
-                        if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
-#else
-                        const float4* nd = s.nodes + 4 * (size_t)cur;
-                        float4 a = nd[0], bb = nd[1], c = nd[2];
-                        uint4 m = *reinterpret_cast<const uint4*>(nd + 3);
-                        const float tmc = tMax * 1.000001f;
-                        float zloL, zloR;
-                        bool hL = box_fast<ID>(r, a.x, a.y, a.z, a.w, bb.x, bb.y, zloL);
-                        bool hR = box_fast<ID>(r, bb.z, bb.w, c.x, c.y, c.z, c.w, zloR);
-                        if (r.cull_ok()) {
-                            if (zloL > tmc && zloL > 1e-20f) hL = false;
-                            if (zloR > tmc && zloR > 1e-20f) hR = false;
-                        }
-                        bool rightFirst = comp(r.d, (int)m.z) < 0;     // :448
-                        uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
-                        bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
-                        float zFar = rightFirst ? zloL : zloR;
-                        if (hNear && hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
-                        uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
-                        if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
-#endif
-                        cur = go;
+                        busy = 0;
                     }
                 }
-                if (done) {
-                    const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
-                    if (WF_DIAG_NOSTORE) {
-                        // timing experiment only: results are dropped
-                    } else if (WF_NT) {
-                        if (kind == 2) __builtin_nontemporal_store(hitTri, b.hit + p);
-                        else __builtin_nontemporal_store((uint8_t)(hitTri >= 0 ? 1 : 0), b.occ + 2 * (size_t)p + kind);
-                    } else {
-                        if (kind == 2) b.hit[p] = hitTri;
-                        else b.occ[2 * (size_t)p + kind] = hitTri >= 0 ? 1 : 0;
-                    }
-                    busy = 0;
-                }
+                if (__popcll(__ballot(busy != 0)) <= thr) break;
             }
-            if (__popcll(__ballot(busy != 0)) <= thr) break;
-        }
         };
         if (__ballot(busy != 0 && r.kz() != 2) == 0) run(std::true_type{});
         else run(std::false_type{});
@@ -671,26 +575,6 @@ __global__ void __launch_bounds__(256) pt_wf_shade_setup(DevScene s, FrameParams
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, colors, i) : 0u;
     wf_enqueue(b, i, nfl);     // every lane of the wave reaches this point
-}
-
-// BVH2 pass for the rays the wide traversal deferred (non-finite rays): one
-// thread per ray, the primary pass's traverse<>.
-__global__ void __launch_bounds__(256) pt_wf_trace_deferred(DevScene s, WfBufs b, int mode) {
-    const uint32_t cnt = *b.defcount;
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < cnt; q += gridDim.x * blockDim.x) {
-        const uint32_t rid = b.defq[q], kind = rid >> 30, p = rid & 0x3fffffffu;
-        RayP r;
-        float tmax;
-        bool any;
-        wf_load_ray(b, kind, p, mode, r, tmax, any);
-        int hitTri = -1;
-        if (kind == 2) {
-            traverse<false>(s, r, tmax, hitTri);
-            b.hit[p] = hitTri;
-        } else {
-            b.occ[2 * (size_t)p + kind] = traverse<true>(s, r, tmax, hitTri) ? 1 : 0;
-        }
-    }
 }
 
 // Debug/reference variant of pt_wf_trace: one thread per ray, the verified
