@@ -85,6 +85,14 @@ int pnrt_upload_texture(pnrt_ctx* ctx, int slot, const uint8_t* pixels, int widt
 int pnrt_upload_env(pnrt_ctx* ctx, const float* hdr_rgb, const float* random_hdr_rgb, int width,
                     int height);
 
+/* LoadHDRImage (shader.hpp:126-225) with its RandomHDR table built on the
+ * GPU instead of on the host: the same table, bit for bit, as the
+ * host restatement pnrt_hdr_build_table (every float sum in the reference's
+ * order).  hdr_rgb: width*height*3 floats as stbi_loadf returns them. */
+int pnrt_upload_env_build(pnrt_ctx* ctx, const float* hdr_rgb, int width, int height);
+/* Copy the bound RandomHDR table (width*height*3 floats) to the host. */
+int pnrt_read_env_table(pnrt_ctx* ctx, float* random_hdr_out);
+
 /* Replaces the per-frame uniforms SCREEN_WIDTH/HEIGHT (main.cpp:389-390),
  * camera.* (main.cpp:606-610) and MAX_BOUNCE_DEPTH (main.cpp:593,599).
  * (Re)allocates a zeroed width*height RGBA32F accumulation image when the

@@ -17,6 +17,7 @@
 
 #include "pt_path.h"
 #include "pt_wf.h"
+#include "pt_env.h"
 
 __global__ void pt_pack_rows_kernel(const float4* accum, float4* dst, int width, int rows, int band,
                                     int n_shards, int shard) {
@@ -557,6 +558,53 @@ int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int 
     HIPCHK(c, hipMemcpy(c->rnd, b.data(), b.size() * 16, hipMemcpyHostToDevice));
     c->scene.has_hdr = 1;
     c->scene.hdr_w = w; c->scene.hdr_h = h;
+    return PNRT_OK;
+}
+
+int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
+    if (!c) return PNRT_E_ARG;
+    if (!rgb || w <= 0 || h <= 0) return set_err(c, PNRT_E_ARG, "upload_env_build: bad arguments");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(c->hdr); (void)hipFree(c->rnd);
+    c->hdr = c->rnd = nullptr;
+    c->scene.has_hdr = 0;
+    const size_t n = (size_t)w * h;
+    std::vector<float4> a(n);
+    for (size_t i = 0; i < n; ++i) a[i] = make_float4(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], 0.f);
+    HIPCHK(c, hipMalloc(&c->hdr, n * 16));
+    HIPCHK(c, hipMalloc(&c->rnd, n * 16));
+    HIPCHK(c, hipMemcpy(c->hdr, a.data(), n * 16, hipMemcpyHostToDevice));
+    float* tmp = nullptr;                     // lumY/pdfY | lumX | cdfY | marginX | cdfX | sum
+    HIPCHK(c, hipMalloc(&tmp, (3 * n + 2 * (size_t)w + 64) * 4));
+    float *pdfY = tmp, *lumX = tmp + n, *cdfY = tmp + 2 * n, *marginX = tmp + 3 * n, *cdfX = marginX + w,
+          *sum = cdfX + w;
+    const unsigned gp = (unsigned)((n + 255) / 256), gx = (unsigned)((w + 255) / 256);
+    hipLaunchKernelGGL(env_lumen_kernel, dim3(gp), dim3(256), 0, c->stream, (const float4*)c->hdr, pdfY, lumX, w, h);
+    hipLaunchKernelGGL(env_sum_kernel, dim3(1), dim3(64), 0, c->stream, (const float*)lumX, n, sum);
+    hipLaunchKernelGGL(env_margin_kernel, dim3(gx), dim3(256), 0, c->stream, pdfY, (const float*)sum, marginX, w, h);
+    hipLaunchKernelGGL(env_cdfx_kernel, dim3(1), dim3(64), 0, c->stream, (const float*)marginX, cdfX, w);
+    hipLaunchKernelGGL(env_cdfy_kernel, dim3(gx), dim3(256), 0, c->stream, (const float*)pdfY, (const float*)marginX, cdfY, w, h);
+    hipLaunchKernelGGL(env_table_kernel, dim3(gp), dim3(256), 0, c->stream, (const float*)cdfX, (const float*)cdfY,
+                       (const float*)pdfY, static_cast<float4*>(c->rnd), w, h);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return set_err(c, PNRT_E_HIP, std::string("upload_env_build: ") + hipGetErrorString(e));
+    c->scene.has_hdr = 1;
+    c->scene.hdr_w = w; c->scene.hdr_h = h;
+    return PNRT_OK;
+}
+
+int pnrt_read_env_table(pnrt_ctx* c, float* out) {
+    if (!c || !out) return PNRT_E_ARG;
+    if (!c->rnd) return set_err(c, PNRT_E_STATE, "read_env_table: no environment");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t n = (size_t)c->scene.hdr_w * c->scene.hdr_h;
+    std::vector<float4> t(n);
+    HIPCHK(c, hipMemcpy(t.data(), c->rnd, n * 16, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; ++i) { out[3 * i] = t[i].x; out[3 * i + 1] = t[i].y; out[3 * i + 2] = t[i].z; }
     return PNRT_OK;
 }
 

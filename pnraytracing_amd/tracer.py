@@ -71,6 +71,19 @@ class PathTracer:
         h, w = rgb.shape[:2]
         self._ck(self._lib.pnrt_upload_env(self._ctx, N.fptr(rgb), N.fptr(table), w, h), "pnrt_upload_env")
 
+    def upload_env_build(self, rgb: np.ndarray):
+        """Environment with its RandomHDR table built on the GPU (pt_env.h)."""
+        rgb = np.ascontiguousarray(rgb, np.float32)
+        h, w = rgb.shape[:2]
+        self._ck(self._lib.pnrt_upload_env_build(self._ctx, N.fptr(rgb), w, h), "pnrt_upload_env_build")
+        self._env_shape = (h, w)
+
+    def read_env_table(self) -> np.ndarray:
+        h, w = self._env_shape
+        out = np.empty((h, w, 3), np.float32)
+        self._ck(self._lib.pnrt_read_env_table(self._ctx, N.fptr(out)), "pnrt_read_env_table")
+        return out
+
     def set_frame(self, width: int, height: int, camera: np.ndarray, max_depth: int = 4):
         cam = N.Camera()
         c = np.asarray(camera, np.float32).reshape(4, 3)

@@ -1,0 +1,24 @@
+"""Accumulation-image output (display conversion, PNG, PFM)."""
+import numpy as np
+
+from pnraytracing_amd import image
+
+
+def test_display_conversion():
+    acc = np.zeros((2, 3, 4), np.float32)
+    acc[0, 0, :3] = (0.5, 1.5, -1.0)        # bottom row in GL
+    acc[1, 2, :3] = (1 / 255, 0.25, 0.999)
+    d = image.to_display(acc)
+    assert d.shape == (2, 3, 3) and d.dtype == np.uint8
+    assert d[1, 0].tolist() == [128, 255, 0]  # flipped to the last (bottom) row
+    assert d[0, 2].tolist() == [1, 64, 255]
+
+
+def test_png_and_pfm_round_trip(tmp_path):
+    from PIL import Image
+    rng = np.random.default_rng(1)
+    acc = rng.random((17, 23, 4)).astype(np.float32)
+    image.write_png(str(tmp_path / "a.png"), acc)
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "a.png")), image.to_display(acc))
+    image.write_pfm(str(tmp_path / "a.pfm"), acc)
+    assert np.array_equal(image.read_pfm(str(tmp_path / "a.pfm")).view(np.uint32), acc[..., :3].view(np.uint32))
