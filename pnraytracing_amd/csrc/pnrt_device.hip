@@ -91,8 +91,6 @@ struct pnrt_ctx {
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
     double prof_ms[PNRT_K_COUNT] = {};
     int64_t prof_n[PNRT_K_COUNT] = {};
-    bool debug_simple_trace = false;
-    int debug_variant = 0;
 };
 
 static int set_err(pnrt_ctx* c, int code, const std::string& m) {
@@ -190,11 +188,11 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
-    const size_t per_path = 16 * 11 + 4 + 4 + 2 + 12 + 1;  // S0-3,S5, C0-3, R0-1 | flags | hit | occ | ray queues | counts
+    const size_t per_path = 16 * 9 + 4 + 4 + 2 + 96 + 1;  // S0-3,S5, C0-3 | flags | hit | occ | 3 ray records | counts
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, &c->wf, &c->wf_cap, nmax * per_path + 8192)) ||
+        (rc = grow(c, &c->wf, &c->wf_cap, (nmax + 256) * per_path + 65536)) ||   // npad rounding + alignment
         (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8)))
         return rc;
     {
@@ -208,7 +206,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         WfBufs b;
         size_t n = (size_t)tiles_x * tiles_y * 64 * cf;
         char* base = static_cast<char*>(c->wf);
-        float4** f4[] = {&b.S0, &b.S1, &b.S2, &b.S3, &b.S5, &b.C0, &b.C1, &b.C2, &b.C3, &b.R0, &b.R1};
+        float4** f4[] = {&b.S0, &b.S1, &b.S2, &b.S3, &b.S5, &b.C0, &b.C1, &b.C2, &b.C3};
         size_t off = 0;
         for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
         b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
@@ -217,7 +215,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         off = (off + 255) & ~(size_t)255;
         b.npad = (uint32_t)((n + 255) / 256 * 256);
         b.nseg_k = b.npad / 256;
-        b.rayq = reinterpret_cast<uint32_t*>(base + off); off += (size_t)b.npad * 12;
+        b.rayO = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
+        b.rayD = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
         b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
         off = (off + 255) & ~(size_t)255;
         off = (off + 255) & ~(size_t)255;
@@ -241,15 +240,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
             HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 32, c->stream));
             {
                 ProfScope ps(c, PNRT_K_TRACE);
-                if (c->debug_simple_trace)
-                    hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b,
-                                       fp.mode);
-                else if (c->debug_variant == 1)   // deep LDS stack, no spill
-                    hipLaunchKernelGGL((pt_wf_trace<48, false>), dim3(256), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
-                else if (c->debug_variant == 2)   // refill only when every lane is idle
-                    hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
-                else
-                    hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream, s, b, fp.mode);
+                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream,
+                                   s, b, fp.mode);
             }
             HIPCHK(c, hipGetLastError());
             if (WF_STATS) {
@@ -259,32 +251,6 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
                 fprintf(stderr, "[trace stats] bounce %d n=%zu iters=%llu active/iter=%.1f tri=%llu node=%llu pop-only=%llu "
                         "refills=%llu rays=%llu  lane-steps/ray=%.1f\n", bounce, n, st[0], st[0] ? (double)st[1] / st[0] : 0.0,
                         st[2], st[3], st[4], st[5], st[6], st[6] ? (double)st[1] / st[6] : 0.0);
-            }
-            if (c->debug_variant == 9) {   // compare every ray with the simple kernel
-                std::vector<int> h1(n), h2(n);
-                std::vector<uint8_t> o1(2 * n), o2(2 * n);
-                std::vector<uint32_t> fl(n);
-                HIPCHK(c, hipStreamSynchronize(c->stream));
-                HIPCHK(c, hipMemcpy(h1.data(), b.hit, n * 4, hipMemcpyDeviceToHost));
-                HIPCHK(c, hipMemcpy(o1.data(), b.occ, 2 * n, hipMemcpyDeviceToHost));
-                HIPCHK(c, hipMemcpy(fl.data(), b.flags, n * 4, hipMemcpyDeviceToHost));
-                hipLaunchKernelGGL(pt_wf_trace_simple, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, c->stream, s, b, fp.mode);
-                HIPCHK(c, hipStreamSynchronize(c->stream));
-                HIPCHK(c, hipMemcpy(h2.data(), b.hit, n * 4, hipMemcpyDeviceToHost));
-                HIPCHK(c, hipMemcpy(o2.data(), b.occ, 2 * n, hipMemcpyDeviceToHost));
-                size_t bad[3] = {0, 0, 0}, tot[3] = {0, 0, 0};
-                long first[3] = {-1, -1, -1};
-                for (size_t p = 0; p < n; ++p) {
-                    if (!(fl[p] & WF_ALIVE)) continue;
-                    if (fl[p] & WF_RLIGHT) { tot[0]++; if (o1[2 * p] != o2[2 * p]) { if (first[0] < 0) first[0] = (long)p; bad[0]++; } }
-                    if (fl[p] & WF_RENV) { tot[1]++; if (o1[2 * p + 1] != o2[2 * p + 1]) { if (first[1] < 0) first[1] = (long)p; bad[1]++; } }
-                    if (fl[p] & WF_RCONT) { tot[2]++; if (h1[p] != h2[p]) { if (first[2] < 0) first[2] = (long)p; bad[2]++; } }
-                }
-                fprintf(stderr, "[trace check] bounce %d: light %zu/%zu env %zu/%zu cont %zu/%zu mismatches; first p=%ld/%ld/%ld",
-                        bounce, bad[0], tot[0], bad[1], tot[1], bad[2], tot[2], first[0], first[1], first[2]);
-                if (first[0] >= 0) fprintf(stderr, " light p%ld persistent=%d simple=%d", first[0], o1[2 * first[0]], o2[2 * first[0]]);
-                if (first[2] >= 0) fprintf(stderr, " cont p%ld persistent=%d simple=%d", first[2], h1[first[2]], h2[first[2]]);
-                fprintf(stderr, "\n");
             }
             {
                 ProfScope ps(c, PNRT_K_SHADE);
@@ -319,12 +285,6 @@ int pnrt_create(int device, pnrt_ctx** out) {
         return PNRT_E_HIP;
     }
     c->stream = c->own_stream;
-    {
-        const char* e = getenv("PNRT_DEBUG_SIMPLE_TRACE");
-        c->debug_simple_trace = e && e[0] == '1';
-        const char* v = getenv("PNRT_DEBUG_TRACE_VARIANT");
-        c->debug_variant = v ? atoi(v) : 0;
-    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_sobolV), kSobolV, sizeof kSobolV) != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;

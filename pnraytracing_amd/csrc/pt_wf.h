@@ -45,8 +45,6 @@ struct WfBufs {
     float4* C1;   // LEnvironment.xyz, enPDF
     float4* C2;   // dBRDF.xyz, |N.L|
     float4* C3;   // L.xyz, dPDF
-    float4* R0;   // light shadow direction (unnormalised), -
-    float4* R1;   // env shadow direction, -
     // trace results
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
@@ -54,9 +52,11 @@ struct WfBufs {
     uint32_t ovf_stride;
     unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
     // ray queues, written by setup without atomics: setup block j compacts its
-    // paths' rays of kind k into segment (k, j) = rayq[k * npad + 256 j ...]
-    // and stores the count in segcount[k * nseg_k + j]
-    uint32_t* rayq;          // [3 * npad] path slots
+    // paths' rays of kind k (light | env | continuation) into segment (k, j) =
+    // slots [k * npad + 256 j, +segcount[k * nseg_k + j]) as ready-to-trace
+    // records: rayO = (origin, bits(path slot)), rayD = (direction, -)
+    float4* rayO;            // [3 * npad]
+    float4* rayD;            // [3 * npad]
     unsigned int* segcount;  // [3 * nseg_k]
     uint32_t npad;           // n rounded up to 256
     uint32_t nseg_k;         // setup blocks = segments per kind
@@ -94,10 +94,17 @@ struct PathIn {
 };
 
 // ---- setup: one bounce's sampling and BRDF values (ray_tracing.comp:866-934) -----------------
+// The bounce's three rays (:886-889 light: origin P + N*1e-4, unnormalised
+// direction; :917-920 env: origin P; :949 continuation: origin P + N*1e-4).
+struct BounceRays {
+    f3 oOff, oP;          // offset origin, plain origin
+    f3 dL, dE, dC;
+};
+
 // Returns the path's flags for the bounce (alive, bounce, which rays exist);
-// writes the bounce candidates C0-C3, shadow directions R0/R1, S3 and flags.
+// writes the bounce candidates C0-C3, S3 and flags; the rays go to `rays`.
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, int bounce,
-                              int x, int py, uint32_t frame, const PathIn& q) {
+                              int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const f3 P = q.P, N = q.N, V = q.V;
     const int hmat = q.mt & 0x00ffffff, htex = (int)((uint32_t)q.mt >> 24) - 1;
     uint32_t seed = q.seed;
@@ -138,7 +145,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         f3 li = get_emissive(s, lmat);
         f3 lightBRDF = disney(bc, lightL);
         LD = divs(muls(mul(lightBRDF, li), pnm_fabs(dot(N, lightL))), pl);
-        b.R0[i] = make_float4(ldir.x, ldir.y, ldir.z, 0.f);
+        rays.dL = ldir;
         nfl |= WF_RLIGHT;
     }
     // environment (:911-926)
@@ -151,7 +158,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         if (dot(enL, N) > 0) {
             f3 dB = disney(bc, enL);
             LE = divs(muls(mul(dB, enLi), dot(enL, N)), pe);
-            b.R1[i] = make_float4(enL.x, enL.y, enL.z, 0.f);
+            rays.dE = enL;
             nfl |= WF_RENV;
         }
     }
@@ -206,34 +213,53 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     b.C3[i] = make_float4(L.x, L.y, L.z, dPDF);
     b.S3[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(seed));
     b.flags[i] = nfl | WF_RCONT;
+    rays.dC = L;
+    rays.oP = P;
+    rays.oOff = add(P, muls(N, 0.0001f));
     return nfl | WF_RCONT;
 }
 
 // Compact the block's rays of each kind into its own queue segment: a ballot
 // per wave, wave offsets through LDS, no global atomics.  Each ray's traversal
 // result is independent of every other ray and of its queue position.
-PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl) {
-    __shared__ unsigned int wcnt[3][4];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt_mask = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+#ifndef WF_SORT_OCTANT
+#define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
+#endif
+PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays) {
+    // Inside a segment the rays are grouped by direction octant: rays with the
+    // same signs take the same near/far choice at every node (:448), so a wave
+    // walks the tree more coherently.  Slots within an octant come from LDS
+    // atomics (order not deterministic, which no result depends on).
+    __shared__ unsigned int bin[3][9];
     const uint32_t need[3] = {WF_RLIGHT, WF_RENV, WF_RCONT};
-    uint64_t m[3];
+    if (threadIdx.x < 27) (&bin[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    int oct[3];
+    unsigned int rank[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        m[k] = __ballot((nfl & need[k]) != 0);
-        if (lane == 0) wcnt[k][wave] = (unsigned int)__popcll(m[k]);
+        const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
+        oct[k] = WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
+        rank[k] = (nfl & need[k]) ? atomicAdd(&bin[k][oct[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {                    // exclusive prefix over the octants of a kind
+        unsigned int run = 0;
+        for (int o = 0; o < 8; ++o) { const unsigned int c = bin[threadIdx.x][o]; bin[threadIdx.x][o] = run; run += c; }
+        bin[threadIdx.x][8] = run;
+        b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] = run;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        unsigned int off = 0;
-        for (int w = 0; w < wave; ++w) off += wcnt[k][w];
-        if (nfl & need[k])
-            b.rayq[(size_t)k * b.npad + (size_t)blockIdx.x * 256 + off + (uint32_t)__popcll(m[k] & lt_mask)] = i;
+        if (nfl & need[k]) {
+            const size_t slot = (size_t)k * b.npad + (size_t)blockIdx.x * 256 + bin[k][oct[k]] + rank[k];
+            const f3 o = k == 1 ? rays.oP : rays.oOff;
+            const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
+            b.rayO[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(i));
+            b.rayD[slot] = make_float4(d.x, d.y, d.z, 0.f);
+        }
     }
-    if (threadIdx.x < 3)
-        b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] =
-            wcnt[threadIdx.x][0] + wcnt[threadIdx.x][1] + wcnt[threadIdx.x][2] + wcnt[threadIdx.x][3];
 }
 
 // ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
@@ -241,6 +267,7 @@ __global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams f
                                                        float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t nfl = 0;
+    BounceRays rays;
     if (i < b.n) {
         int x, lr, k;
         wf_coords(b, i, x, lr, k);
@@ -267,11 +294,11 @@ __global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams f
                 b.S1[i] = make_float4(q.N.x, q.N.y, q.N.z, q.v);
                 b.S2[i] = make_float4(0.f, 0.f, 0.f, __int_as_float(mt));
                 b.S5[i] = make_float4(base.x, base.y, base.z, 0.f);
-                nfl = wf_setup_core(s, fp, b, i, 0, x, py, frame, q);
+                nfl = wf_setup_core(s, fp, b, i, 0, x, py, frame, q, rays);
             }
         }
     }
-    wf_enqueue(b, i, nfl);     // every lane of the wave reaches this point
+    wf_enqueue(b, i, nfl, rays);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
@@ -336,15 +363,14 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
 
-// Load ray (kind, path p) of the bounce into a lane.
-PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t p, int mode, RayP& r, float& tmax, bool& any) {
-    float4 s0 = b.S0[p], s1 = b.S1[p];
-    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
-    float4 dv = kind == 0 ? b.R0[p] : (kind == 1 ? b.R1[p] : b.C3[p]);
-    f3 o = kind == 1 ? P : add(P, muls(N, 0.0001f));
+// Ray record `slot` of a kind-`kind` segment -> lane ray state.
+PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
+                        uint32_t& p) {
+    const float4 ro = b.rayO[slot], rd = b.rayD[slot];
+    p = __float_as_uint(ro.w);
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
-    r = make_ray(o, mk3(dv.x, dv.y, dv.z), mode);
+    r = make_ray(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), mode);
 }
 
 // Persistent traversal of every queued ray of the bounce.
@@ -404,11 +430,12 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 const uint32_t myid = next + lanes_below(idle);
                 next = min(next + (uint32_t)__popcll(idle), end);
                 if (busy == 0 && myid < end) {
-                    const uint32_t kind = ckind, p = b.rayq[myid];
+                    const uint32_t kind = ckind;
+                    uint32_t p;
                     RayP nr;
                     float ntmax;
                     bool nany;
-                    wf_load_ray(b, kind, p, mode, nr, ntmax, nany);
+                    wf_load_ray(b, kind, myid, mode, nr, ntmax, nany, p);
                     float zlo;
                     uint32_t root = REF_NONE;
                     int nlt = 0, nlc = 0;
@@ -514,7 +541,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 }
 
 // ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
-PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, float4* colors, uint32_t i) {
+PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, float4* colors, uint32_t i,
+                              BounceRays& rays) {
     const uint32_t fl = b.flags[i];
     if (!(fl & WF_ALIVE)) return 0;
     int bounce = (int)((fl >> 8) & 7u);
@@ -566,39 +594,14 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
     q.P = h.P; q.N = h.N; q.u = h.u; q.v = h.v; q.mt = mt;
     q.V = neg(L); q.cw = cw; q.seed = __float_as_uint(s3.w);
     const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
-    return wf_setup_core(s, fp, b, i, bounce, x, py, b.first_frame + (uint32_t)k, q);
+    return wf_setup_core(s, fp, b, i, bounce, x, py, b.first_frame + (uint32_t)k, q, rays);
 }
 
 // ---- shade + next-bounce setup: MIS, continuation hit (:936-972), then the next
 // bounce's sampling for the paths that continue ----------------------------------------------
 __global__ void __launch_bounds__(256) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b, float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, colors, i) : 0u;
-    wf_enqueue(b, i, nfl);     // every lane of the wave reaches this point
-}
-
-// Debug/reference variant of pt_wf_trace: one thread per ray, the verified
-// traverse<> of the primary pass (selected with PNRT_DEBUG_SIMPLE_TRACE=1).
-__global__ void __launch_bounds__(256) pt_wf_trace_simple(DevScene s, WfBufs b, int mode) {
-    uint32_t myid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (myid >= 3u * b.n) return;
-    const uint32_t kind = myid / b.n, p = myid - kind * b.n;
-    uint32_t fl = b.flags[p];
-    uint32_t need = kind == 0 ? WF_RLIGHT : (kind == 1 ? WF_RENV : WF_RCONT);
-    if (!((fl & WF_ALIVE) && (fl & need))) return;
-    float4 s0 = b.S0[p], s1 = b.S1[p];
-    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
-    f3 o, d;
-    float tmax;
-    if (kind == 0) { float4 r = b.R0[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = 1.0f - PT_SHADOW_EPS; }
-    else if (kind == 1) { float4 r = b.R1[p]; o = P; d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
-    else { float4 r = b.C3[p]; o = add(P, muls(N, 0.0001f)); d = mk3(r.x, r.y, r.z); tmax = PT_FLOAT_MAX; }
-    RayP r = make_ray(o, d, mode);
-    int hitTri = -1;
-    if (kind == 2) {
-        traverse<false>(s, r, tmax, hitTri);
-        b.hit[p] = hitTri;
-    } else {
-        b.occ[2 * (size_t)p + kind] = traverse<true>(s, r, tmax, hitTri) ? 1 : 0;
-    }
+    BounceRays rays;
+    const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, colors, i, rays) : 0u;
+    wf_enqueue(b, i, nfl, rays);     // every lane of the wave reaches this point
 }
