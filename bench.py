@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-image", default="")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     return ap.parse_args()
 
 
@@ -96,9 +98,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:          # rehearsal of N ranks on fewer GPUs (gloo only)
+        if args.backend == "nccl":
+            raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPU(s): RCCL needs one GPU per rank")
+        local = local % ndev
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from pnraytracing_amd import scenes
     from pnraytracing_amd.dist import ShardedFrame
@@ -148,7 +158,7 @@ def main():
     k_ms_total, k_launches = prof[kname]
     kern_ms = k_ms_total / max(k_launches, 1)                  # average launch duration
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 

@@ -39,13 +39,19 @@ class ShardedFrame:
         H, W = tracer.height, tracer.width
         if H <= 0 or W <= 0:
             raise ValueError("ShardedFrame: set_frame() the tracer first")
+        # gloo cannot gather device tensors: stage through host memory (rehearsal
+        # of the multi-GPU path on one GPU / CPU-only hosts); RCCL gathers in HBM
+        self.stage = (dist.is_initialized() and self.device.type == "cuda"
+                      and dist.get_backend(group) == "gloo")
         rows = [shard_rows(H, band, self.world, r) for r in range(self.world)]
         self.rows = [torch.as_tensor(r, device=self.device) for r in rows]
         self.my_rows = len(rows[self.rank])
         self.max_rows = max(len(r) for r in rows)           # rank 0 owns the most (first bands)
         # equal-sized buffers for the collective; the tail of a short shard is padding
         self.send = torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=self.device)
-        self.recv = [torch.zeros_like(self.send) for _ in range(self.world)] if self.rank == 0 else None
+        cdev = torch.device("cpu") if self.stage else self.device
+        self.recv = [torch.zeros(self.send.shape, dtype=torch.float32, device=cdev) for _ in range(self.world)] \
+            if self.rank == 0 else None
         self.image = torch.zeros((H, W, 4), dtype=torch.float32, device=self.device) if self.rank == 0 else None
         if self.device.type == "cuda" and hasattr(tracer, "set_stream"):
             tracer.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
@@ -62,13 +68,14 @@ class ShardedFrame:
         if self.world == 1:
             self.image.copy_(self.send)
             return self.image
-        dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0, group=self.group)
+        send = self.send.cpu() if self.stage else self.send
+        dist.gather(send, self.recv if self.rank == 0 else None, dst=0, group=self.group)
         if self.rank != 0:
             return None
         for r in range(self.world):
             n = len(self.rows[r])
             if n:
-                self.image.index_copy_(0, self.rows[r], self.recv[r][:n])
+                self.image.index_copy_(0, self.rows[r], self.recv[r][:n].to(self.device, non_blocking=False))
         return self.image
 
 
