@@ -142,6 +142,19 @@ typedef struct {
 int pnrt_profile_enable(pnrt_ctx* ctx, int on);
 int pnrt_profile_read(pnrt_ctx* ctx, pnrt_profile* out);
 
+/* GPU BuildBVH: the reference's binned-SAH build
+ * (include/BVH.hpp:92-173, called from the BVH ctor :16-19 via main.cpp's
+ * scene setup) run on the device, returning the SAME node array (pre-order,
+ * main.cpp:488-501 layout, 12 floats per node) and the SAME triangle order as
+ * the host build, bit for bit.  Input per triangle, in the current order: its
+ * Bound and boundCenter (triangle.hpp:11-12) as 9 floats pMin.xyz pMax.xyz
+ * centre.xyz.  Output: order_out[i] = input index of the triangle at BVH
+ * position i; nodes_out needs room for 2 * n_triangles - 1 nodes.  Stateless
+ * with respect to the scene (the caller packs and uploads as usual).  Bounds
+ * must be finite; synchronous. */
+int pnrt_bvh_build(pnrt_ctx* ctx, const float* tri_bounds9, int n_triangles, float* nodes_out,
+                   int node_capacity, int* n_nodes_out, int32_t* order_out, int* max_depth_out);
+
 /* Test hook: evaluate one PN-libm / IEEE primitive on the device (same fn
  * codes as the oracle's pno_math_eval); host in/out arrays of n floats. */
 int pnrt_debug_math(pnrt_ctx* ctx, int fn, const float* a, const float* b, float* out, int n);

@@ -7,7 +7,8 @@
  *   reference interface replaced             here
  *   ----------------------------------------  ------------------------------
  *   Model ctor + ModelOutput (model.hpp:22-135) pnrt_scene_add_material/_mesh
- *   BVH::BuildBVH (BVH.hpp:92-173)             pnrt_scene_build
+ *   BVH::BuildBVH (BVH.hpp:92-173)             pnrt_scene_build (or libpnrt.so
+ *                                              pnrt_bvh_build + pnrt_scene_set_bvh)
  *   light prefix list (main.cpp:374-383)       pnrt_scene_build
  *   packing loops (main.cpp:409-524)           pnrt_scene_pack
  *   Camera::UpdateCamera (camera.hpp:11-31)    pnrt_camera_update
@@ -62,6 +63,18 @@ int pnrt_scene_add_mesh(pnrt_scene* s, int material_id, int texture_id,
                         const int32_t* indices, int n_indices);
 /* BuildBVH over all triangles + emissive light list. */
 int pnrt_scene_build(pnrt_scene* s);
+/* GPU BuildBVH support (libpnrt.so pnrt_bvh_build): the builder's input,
+ * Bound + boundCenter of every triangle in the current order (9 floats:
+ * pMin.xyz pMax.xyz centre.xyz), and installing its output (triangle order,
+ * main.cpp-layout nodes) in place of pnrt_scene_build's; the light list is
+ * rebuilt in the new order as pnrt_scene_build does. */
+int pnrt_scene_tri_bounds(const pnrt_scene* s, float* out9);
+int pnrt_scene_set_bvh(pnrt_scene* s, const int32_t* order, const float* bvh_nodes12, int n_nodes,
+                       int max_depth);
+/* The host BuildBVH over bare bounds, with pnrt_bvh_build's signature (no
+ * context): the CPU counterpart the GPU build is checked against. */
+int pnrt_bvh_build_cpu(const float* tri_bounds9, int n_triangles, float* nodes_out, int node_capacity,
+                       int* n_nodes_out, int32_t* order_out, int* max_depth_out);
 typedef struct {
     int n_vertices, n_materials, n_triangles, n_nodes, n_lights;
     float lights_sum_area;

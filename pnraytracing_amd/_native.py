@@ -110,6 +110,9 @@ def _type_host(lib):
     _sig(lib, "pnrt_scene_build", INT, P)
     _sig(lib, "pnrt_scene_get_info", INT, P, ctypes.POINTER(SceneInfo))
     _sig(lib, "pnrt_scene_pack", INT, P, F, F, F, F, F)
+    _sig(lib, "pnrt_scene_tri_bounds", INT, P, F)
+    _sig(lib, "pnrt_scene_set_bvh", INT, P, I32, F, INT, INT)
+    _sig(lib, "pnrt_bvh_build_cpu", INT, F, INT, F, INT, PINT, I32, PINT)
     _sig(lib, "pnrt_camera_update", INT, F, F, F, ctypes.c_float, ctypes.c_float, F)
     _sig(lib, "pnrt_hdr_decode_rgbe", INT, U8, ctypes.c_int64, PINT, PINT, F)
     _sig(lib, "pnrt_hdr_build_table", INT, F, INT, INT, F)
@@ -143,6 +146,7 @@ def _type_device(lib):
     _sig(lib, "pnrt_upload_env_build", INT, P, F, INT, INT)
     _sig(lib, "pnrt_read_env_table", INT, P, F)
     _sig(lib, "pnrt_profile_read", INT, P, ctypes.POINTER(Profile))
+    _sig(lib, "pnrt_bvh_build", INT, P, F, INT, F, INT, PINT, I32, PINT)
 
 
 def fptr(a) -> ctypes.POINTER(ctypes.c_float):

@@ -349,17 +349,8 @@ int pnrt_scene_add_mesh(pnrt_scene* s, int material_id, int texture_id, const fl
     return 0;
 }
 
-int pnrt_scene_build(pnrt_scene* s) {
-    if (!s) return fail(-1, "build: null");
-    if (s->triangles.empty()) return fail(-2, "build: scene has no triangles");
-    for (const Tri& t : s->triangles)
-        if (t.materialId < 0 || t.materialId >= (int)s->materials.size())
-            return fail(-3, "build: triangle references an unknown material");
-    BvhBuilder b(s->triangles);
-    b.build();
-    s->nodes = std::move(b.nodes);
-    s->maxDepth = b.maxDepth;
-    // main.cpp:374-383: emissive triangles in BVH order, float prefix of areas
+// main.cpp:374-383: emissive triangles in BVH order, float prefix of areas
+static void build_lights(pnrt_scene* s) {
     s->lights.clear();
     for (int i = 0; i < (int)s->triangles.size(); ++i) {
         const Tri& t = s->triangles[i];
@@ -370,6 +361,92 @@ int pnrt_scene_build(pnrt_scene* s) {
             if (n > 1) s->lights[n - 1].second += s->lights[n - 2].second;
         }
     }
+}
+
+static int check_buildable(pnrt_scene* s, const char* who) {
+    if (!s) return fail(-1, std::string(who) + ": null");
+    if (s->triangles.empty()) return fail(-2, std::string(who) + ": scene has no triangles");
+    for (const Tri& t : s->triangles)
+        if (t.materialId < 0 || t.materialId >= (int)s->materials.size())
+            return fail(-3, std::string(who) + ": triangle references an unknown material");
+    return 0;
+}
+
+int pnrt_scene_build(pnrt_scene* s) {
+    if (int rc = check_buildable(s, "build")) return rc;
+    BvhBuilder b(s->triangles);
+    b.build();
+    s->nodes = std::move(b.nodes);
+    s->maxDepth = b.maxDepth;
+    build_lights(s);
+    s->built = true;
+    return 0;
+}
+
+int pnrt_scene_tri_bounds(const pnrt_scene* s, float* out) {
+    if (!s || !out) return fail(-1, "tri_bounds: null");
+    size_t k = 0;
+    for (const Tri& t : s->triangles) {
+        out[k++] = t.bound.pMin.x; out[k++] = t.bound.pMin.y; out[k++] = t.bound.pMin.z;
+        out[k++] = t.bound.pMax.x; out[k++] = t.bound.pMax.y; out[k++] = t.bound.pMax.z;
+        out[k++] = t.boundCenter.x; out[k++] = t.boundCenter.y; out[k++] = t.boundCenter.z;
+    }
+    return 0;
+}
+
+int pnrt_bvh_build_cpu(const float* tb, int n, float* nodes_out, int cap, int* n_nodes_out, int32_t* order_out,
+                       int* max_depth_out) {
+    if (!tb || n <= 0 || !nodes_out || !n_nodes_out || !order_out) return fail(-1, "bvh_build_cpu: bad arguments");
+    std::vector<Tri> t(n);
+    for (int i = 0; i < n; ++i) {
+        const float* q = tb + 9 * (size_t)i;
+        t[i].bound.pMin = vec3(q[0], q[1], q[2]);
+        t[i].bound.pMax = vec3(q[3], q[4], q[5]);
+        t[i].boundCenter = vec3(q[6], q[7], q[8]);
+        t[i].indices[0] = i;                  // carries the input index through std::partition
+    }
+    BvhBuilder b(t);
+    b.build();
+    if ((int)b.nodes.size() > cap) return fail(-2, "bvh_build_cpu: node capacity exceeded");
+    for (size_t i = 0; i < b.nodes.size(); ++i) {
+        const Node& d = b.nodes[i];
+        float* q = nodes_out + 12 * i;
+        q[0] = d.bound.pMin.x; q[1] = d.bound.pMin.y; q[2] = d.bound.pMin.z;
+        q[3] = d.bound.pMax.x; q[4] = d.bound.pMax.y; q[5] = d.bound.pMax.z;
+        q[6] = (float)d.axis; q[7] = (float)d.rightChild; q[8] = (float)d.startIndex; q[9] = (float)d.endIndex;
+        q[10] = 0.f; q[11] = 0.f;
+    }
+    for (int i = 0; i < n; ++i) order_out[i] = t[i].indices[0];
+    *n_nodes_out = (int)b.nodes.size();
+    if (max_depth_out) *max_depth_out = b.maxDepth;
+    return 0;
+}
+
+int pnrt_scene_set_bvh(pnrt_scene* s, const int32_t* order, const float* nb, int n_nodes, int max_depth) {
+    if (int rc = check_buildable(s, "set_bvh")) return rc;
+    const int n = (int)s->triangles.size();
+    if (!order || !nb || n_nodes <= 0 || n_nodes > 2 * n - 1) return fail(-4, "set_bvh: bad arguments");
+    std::vector<char> seen(n, 0);
+    for (int i = 0; i < n; ++i) {
+        if (order[i] < 0 || order[i] >= n || seen[order[i]]) return fail(-5, "set_bvh: order is not a permutation");
+        seen[order[i]] = 1;
+    }
+    std::vector<Tri> t(n);
+    for (int i = 0; i < n; ++i) t[i] = s->triangles[order[i]];
+    std::vector<Node> nodes(n_nodes);
+    for (int i = 0; i < n_nodes; ++i) {
+        const float* q = nb + 12 * (size_t)i;
+        Node& d = nodes[i];
+        d.bound.pMin = vec3(q[0], q[1], q[2]);
+        d.bound.pMax = vec3(q[3], q[4], q[5]);
+        d.axis = (int)q[6]; d.rightChild = (int)q[7]; d.startIndex = (int)q[8]; d.endIndex = (int)q[9];
+        if (d.startIndex < 0 || d.endIndex > n || d.startIndex > d.endIndex || d.rightChild >= n_nodes)
+            return fail(-6, "set_bvh: node " + std::to_string(i) + " is inconsistent");
+    }
+    s->triangles.swap(t);
+    s->nodes.swap(nodes);
+    s->maxDepth = max_depth;
+    build_lights(s);
     s->built = true;
     return 0;
 }

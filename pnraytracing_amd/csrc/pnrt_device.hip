@@ -6,6 +6,7 @@
 //        -fPIC -shared  (pnraytracing_amd/build.py)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +19,7 @@
 #include "pt_path.h"
 #include "pt_wf.h"
 #include "pt_env.h"
+#include "pt_bvh.h"
 
 __global__ void pt_pack_rows_kernel(const float4* accum, float4* dst, int width, int rows, int band,
                                     int n_shards, int shard) {
@@ -719,3 +721,157 @@ int pnrt_debug_math(pnrt_ctx* c, int fn, const float* a, const float* b, float* 
 }
 
 }  // extern "C"
+
+// ---- GPU BuildBVH (pt_bvh.h) -----------------------------------------------------------------
+namespace {
+struct DevAllocs {                     // device scratch of one build, freed on every return path
+    std::vector<void*> p;
+    ~DevAllocs() { for (void* q : p) (void)hipFree(q); }
+    template <typename T> hipError_t get(T** out, size_t count) {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, count * sizeof(T) + 16);
+        if (e == hipSuccess) { p.push_back(q); *out = static_cast<T*>(q); }
+        return e;
+    }
+};
+}  // namespace
+
+static unsigned blocks_for(long long n, int per) { return (unsigned)((n + per - 1) / per); }
+
+extern "C" int pnrt_bvh_build(pnrt_ctx* c, const float* tb, int n, float* nodes_out, int cap, int* n_nodes_out,
+                              int32_t* order_out, int* max_depth_out) {
+    if (!c) return PNRT_E_ARG;
+    if (!tb || n <= 0 || !nodes_out || !n_nodes_out || !order_out) return set_err(c, PNRT_E_ARG, "bvh_build: bad arguments");
+    if (n >= (1 << 24)) return set_err(c, PNRT_E_ARG, "bvh_build: >= 2^24 triangles cannot be stored as exact floats");
+    if (cap < 2 * n - 1) return set_err(c, PNRT_E_ARG, "bvh_build: node capacity must be >= 2 * n_triangles - 1");
+    HIPCHK(c, hipSetDevice(c->device));
+    // triangle bounds + centres: A = (pMin, cx), B = (pMax, cy), C = cz
+    std::vector<float4> hA(n), hB(n);
+    std::vector<float> hC(n);
+    for (int i = 0; i < n; ++i) {
+        const float* t = tb + 9 * (size_t)i;
+        for (int k = 0; k < 9; ++k)
+            if (!std::isfinite(t[k])) return set_err(c, PNRT_E_SCENE, "bvh_build: triangle " + std::to_string(i) + " has a non-finite bound");
+        hA[i] = make_float4(t[0], t[1], t[2], t[6]);
+        hB[i] = make_float4(t[3], t[4], t[5], t[7]);
+        hC[i] = t[8];
+    }
+    const size_t segcap = (size_t)n / (BVH_SMALL + 1) + 2;
+    const size_t chcap = (size_t)n / BVH_CHUNK + segcap + 2;
+    DevAllocs m;
+    float4 *A, *B; float* C; int *order, *Fpos, *Tpos, *ctrue, *excl;
+    BvhSeg* segs[2]; BvhChunk* chunks[2]; BvhAcc* acc; BvhTop* top; BvhSmall* small; BvhLocal* loc; BvhCtr* ctr;
+    HIPCHK(c, m.get(&A, n)); HIPCHK(c, m.get(&B, n)); HIPCHK(c, m.get(&C, n));
+    HIPCHK(c, m.get(&order, n)); HIPCHK(c, m.get(&Fpos, n)); HIPCHK(c, m.get(&Tpos, n));
+    HIPCHK(c, m.get(&ctrue, chcap)); HIPCHK(c, m.get(&excl, chcap));
+    HIPCHK(c, m.get(&segs[0], segcap)); HIPCHK(c, m.get(&segs[1], segcap));
+    HIPCHK(c, m.get(&chunks[0], chcap)); HIPCHK(c, m.get(&chunks[1], chcap));
+    HIPCHK(c, m.get(&acc, segcap)); HIPCHK(c, m.get(&top, 2 * (size_t)n + 2));
+    HIPCHK(c, m.get(&small, (size_t)n + 1)); HIPCHK(c, m.get(&loc, 2 * (size_t)n + 2));
+    HIPCHK(c, m.get(&ctr, 1));
+    hipStream_t st = c->stream;
+    HIPCHK(c, hipMemcpyAsync(A, hA.data(), n * sizeof(float4), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(B, hB.data(), n * sizeof(float4), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(C, hC.data(), n * sizeof(float), hipMemcpyHostToDevice, st));
+    {
+        std::vector<int> iota(n);
+        for (int i = 0; i < n; ++i) iota[i] = i;
+        HIPCHK(c, hipMemcpyAsync(order, iota.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+    }
+    BvhCtr h{};
+    int nseg = 0, nch = 0, cur = 0;
+    if (n > BVH_SMALL) {                      // root = large range 0 (temporary id 0)
+        BvhSeg s0{}; s0.L = 0; s0.R = n; s0.depth = 0; s0.tmp = 0; s0.chunk0 = 0;
+        std::vector<BvhChunk> ck;
+        for (int p = 0; p < n; p += BVH_CHUNK) ck.push_back({0, p, std::min(p + BVH_CHUNK, n), 0});
+        nseg = 1; nch = (int)ck.size();
+        HIPCHK(c, hipMemcpy(segs[0], &s0, sizeof s0, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(chunks[0], ck.data(), ck.size() * sizeof(BvhChunk), hipMemcpyHostToDevice));
+        h.ntop = 1;
+    } else {                                  // root = small range 0
+        BvhSmall s0{}; s0.L = 0; s0.R = n; s0.depth = 0;
+        HIPCHK(c, hipMemcpy(small, &s0, sizeof s0, hipMemcpyHostToDevice));
+        h.nsmall = 1;
+    }
+    HIPCHK(c, hipMemcpy(ctr, &h, sizeof h, hipMemcpyHostToDevice));
+    int levels = 0;
+    while (nseg > 0) {
+        if (++levels > 100000) return set_err(c, PNRT_E_SCENE, "bvh_build: tree too deep");
+        h.nseg = 0; h.nch = 0;
+        HIPCHK(c, hipMemcpyAsync(ctr, &h, sizeof h, hipMemcpyHostToDevice, st));
+        BvhSeg* sg = segs[cur]; BvhChunk* ck = chunks[cur];
+        const unsigned gs = blocks_for(nseg, 256);
+        hipLaunchKernelGGL(bvh_init_kernel, dim3(gs), dim3(256), 0, st, acc, nseg);
+        hipLaunchKernelGGL(bvh_bounds_kernel, dim3(nch), dim3(256), 0, st, (const BvhChunk*)ck, acc, (const int*)order,
+                           (const float4*)A, (const float4*)B, (const float*)C);
+        hipLaunchKernelGGL(bvh_axis_kernel, dim3(gs), dim3(256), 0, st, (const BvhSeg*)sg, acc, nseg, (const int*)order,
+                           (const float4*)A, (const float4*)B);
+        hipLaunchKernelGGL(bvh_bucket_kernel, dim3(nch), dim3(256), 0, st, (const BvhChunk*)ck, acc, (const int*)order,
+                           (const float4*)A, (const float4*)B, (const float*)C);
+        hipLaunchKernelGGL(bvh_split_kernel, dim3(gs), dim3(256), 0, st, (const BvhSeg*)sg, acc, nseg);
+        hipLaunchKernelGGL(bvh_count_kernel, dim3(nch), dim3(256), 0, st, (const BvhChunk*)ck, (const BvhAcc*)acc,
+                           (const int*)order, (const float4*)A, (const float4*)B, (const float*)C, ctrue);
+        hipLaunchKernelGGL(bvh_scan_kernel, dim3(1), dim3(1024), 0, st, (const int*)ctrue, excl, nch);
+        hipLaunchKernelGGL(bvh_lists_kernel, dim3(nch), dim3(256), 0, st, (const BvhChunk*)ck, (const BvhSeg*)sg, acc,
+                           (const int*)order, (const float4*)A, (const float4*)B, (const float*)C, (const int*)excl,
+                           Fpos, Tpos);
+        hipLaunchKernelGGL(bvh_swap_kernel, dim3(nch), dim3(256), 0, st, (const BvhChunk*)ck, (const BvhSeg*)sg,
+                           (const BvhAcc*)acc, order, (const int*)Fpos, (const int*)Tpos);
+        hipLaunchKernelGGL(bvh_emit_kernel, dim3(gs), dim3(256), 0, st, (const BvhSeg*)sg, (const BvhAcc*)acc, nseg, top,
+                           segs[cur ^ 1], chunks[cur ^ 1], small, ctr);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(&h, ctr, sizeof h, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        nseg = h.nseg; nch = h.nch; cur ^= 1;
+        if ((size_t)nseg > segcap || (size_t)nch > chcap || h.ntop > 2 * n + 2 || h.nsmall > n + 1)
+            return set_err(c, PNRT_E_SCENE, "bvh_build: internal capacity exceeded");
+    }
+    if (h.nsmall > 0) {
+        hipLaunchKernelGGL(bvh_small_kernel, dim3(blocks_for(h.nsmall, 4)), dim3(256), 0, st, small, h.nsmall, order,
+                           (const float4*)A, (const float4*)B, (const float*)C, loc, ctr);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipMemcpyAsync(&h, ctr, sizeof h, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (h.ntop < 0 || h.ntop > 2 * n + 2 || h.nsmall < 0 || h.nsmall > n + 1 || h.small_nodes > 2 * n)
+        return set_err(c, PNRT_E_SCENE, "bvh_build: internal capacity exceeded");
+    std::vector<BvhTop> ht(h.ntop);
+    std::vector<BvhSmall> hs(h.nsmall);
+    if (h.ntop) HIPCHK(c, hipMemcpyAsync(ht.data(), top, h.ntop * sizeof(BvhTop), hipMemcpyDeviceToHost, st));
+    if (h.nsmall) HIPCHK(c, hipMemcpyAsync(hs.data(), small, h.nsmall * sizeof(BvhSmall), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    // pre-order ids (the static nodeId counter of BVH.hpp:94-95): left subtree, then right
+    std::vector<int> ftop(h.ntop + 1, 0), fsmall(h.nsmall + 1, 0);
+    std::vector<int> stk{h.ntop ? 0 : -1};
+    int counter = 0;
+    while (!stk.empty()) {
+        const int ref = stk.back();
+        stk.pop_back();
+        if (ref >= 0) {
+            ftop[ref] = counter++;
+            if (ht[ref].axis != -1) { stk.push_back(ht[ref].right); stk.push_back(ht[ref].left); }
+        } else {
+            fsmall[-ref - 1] = counter;
+            counter += hs[-ref - 1].count;
+        }
+    }
+    if (counter > cap) return set_err(c, PNRT_E_SCENE, "bvh_build: node capacity exceeded");
+    int *dft, *dfs; float* dout;
+    HIPCHK(c, m.get(&dft, ftop.size())); HIPCHK(c, m.get(&dfs, fsmall.size())); HIPCHK(c, m.get(&dout, 12 * (size_t)counter));
+    HIPCHK(c, hipMemcpyAsync(dft, ftop.data(), ftop.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(dfs, fsmall.data(), fsmall.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    if (h.ntop)
+        hipLaunchKernelGGL(bvh_scatter_top_kernel, dim3(blocks_for(h.ntop, 256)), dim3(256), 0, st, (const BvhTop*)top,
+                           h.ntop, (const int*)dft, (const int*)dfs, dout);
+    if (h.nsmall)
+        hipLaunchKernelGGL(bvh_scatter_small_kernel, dim3(blocks_for(h.nsmall, 4)), dim3(256), 0, st,
+                           (const BvhSmall*)small, h.nsmall, (const BvhLocal*)loc, (const int*)dfs, dout);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(nodes_out, dout, 12 * (size_t)counter * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(order_out, order, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    *n_nodes_out = counter;
+    if (max_depth_out) *max_depth_out = h.max_depth;
+    return PNRT_OK;
+}

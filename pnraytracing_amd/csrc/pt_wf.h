@@ -362,6 +362,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
+#ifndef WF_Q3_COND
+#define WF_Q3_COND 0        // node lanes only fetch the refs/axis quarter (triangle lanes skip it)
+#endif
 
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
@@ -477,8 +480,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     float4 q0, q1, q2, q3;
                     if (isTri || cur != REF_NONE) {
                         const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)cur;
-                        q0 = base[0]; q1 = base[1]; q2 = base[2]; q3 = base[3];
+                        q0 = base[0]; q1 = base[1]; q2 = base[2];
+                        if (!WF_Q3_COND) q3 = base[3];
                     }
+                    if (WF_Q3_COND && !isTri && cur != REF_NONE) q3 = s.nodes[4 * (size_t)cur + 3];
                     if (isTri) {
                         float e0, e1, e2, det, ts;
                         if (tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts)) {

@@ -174,6 +174,20 @@ def mesh_teapot() -> Mesh:
     return _mesh_from(N.host_lib().pnrt_mesh_teapot)
 
 
+def bvh_build_cpu(tri_bounds: np.ndarray):
+    """Host BuildBVH (BVH.hpp:92-173) over bare (n, 9) bounds: (nodes, order, max_depth),
+    the same contract as :meth:`pnraytracing_amd.tracer.PathTracer.build_bvh`."""
+    tb = np.ascontiguousarray(tri_bounds, np.float32).reshape(-1, 9)
+    n = len(tb)
+    cap = max(2 * n - 1, 1)
+    nodes = np.empty((cap, 12), np.float32)
+    order = np.empty(n, np.int32)
+    nn, md = ctypes.c_int(), ctypes.c_int()
+    _check(N.host_lib().pnrt_bvh_build_cpu(N.fptr(tb), n, N.fptr(nodes), cap, ctypes.byref(nn), N.iptr(order),
+                                           ctypes.byref(md)), "bvh_build_cpu")
+    return nodes[:nn.value].copy(), order, md.value
+
+
 @dataclasses.dataclass
 class PackedScene:
     """The five arrays main.cpp uploads (texture units 0-4) + uniforms."""
@@ -225,8 +239,27 @@ class SceneBuilder:
         self.models.append((name, mat_id))
         return mat_id
 
-    def build(self) -> PackedScene:
-        _check(self._lib.pnrt_scene_build(self._s), "scene_build")
+    def tri_bounds(self) -> np.ndarray:
+        """(n, 9) per-triangle Bound + boundCenter in the current order (BuildBVH's input)."""
+        info = N.SceneInfo()
+        _check(self._lib.pnrt_scene_get_info(self._s, ctypes.byref(info)), "get_info")
+        out = np.zeros((info.n_triangles, 9), np.float32)
+        _check(self._lib.pnrt_scene_tri_bounds(self._s, N.fptr(out)), "tri_bounds")
+        return out
+
+    def build(self, bvh_tracer=None) -> PackedScene:
+        """BuildBVH + light list + packing.  With ``bvh_tracer`` (a
+        :class:`pnraytracing_amd.tracer.PathTracer`) the BVH is built on its GPU
+        (pnrt_bvh_build) -- the same arrays as the host build, bit for bit."""
+        if bvh_tracer is None:
+            _check(self._lib.pnrt_scene_build(self._s), "scene_build")
+        else:
+            nodes, order, depth = bvh_tracer.build_bvh(self.tri_bounds())
+            _check(self._lib.pnrt_scene_set_bvh(self._s, N.iptr(order), N.fptr(nodes), len(nodes), depth),
+                   "scene_set_bvh")
+        return self._pack()
+
+    def _pack(self) -> PackedScene:
         info = N.SceneInfo()
         _check(self._lib.pnrt_scene_get_info(self._s, ctypes.byref(info)), "get_info")
         V = np.zeros((info.n_vertices, 15), np.float32)

@@ -6,6 +6,9 @@ The reference's meshes (``Bunny.obj``, ``floor.obj``, ``teapot.obj``,
 deterministic procedural stand-in of the same role and size class; the
 Cornell box transforms, materials and cameras are the reference's own
 (main.cpp:198-247, :329-347).
+
+Every builder takes ``bvh_tracer``: a PathTracer whose GPU builds the BVH
+(pnrt_bvh_build) instead of the host library -- the same arrays either way.
 """
 from __future__ import annotations
 
@@ -70,15 +73,15 @@ def _env_1k():
     return H.load_hdr(HDR_1K)
 
 
-def cornell_c1(width=256, height=256, spp=1) -> SceneConfig:
+def cornell_c1(width=256, height=256, spp=1, bvh_tracer=None) -> SceneConfig:
     """C1: Cornell box, 12 triangles, no environment (CPU-oracle config)."""
     sb = H.SceneBuilder()
     _cornell_walls(sb, H.Material(baseColor=(0.65, 0.65, 0.65)))
-    return SceneConfig("C1-cornell", sb.build(), _cornell_camera(width, height), width, height, spp,
+    return SceneConfig("C1-cornell", sb.build(bvh_tracer), _cornell_camera(width, height), width, height, spp,
                        description="Cornell box (12 tris), 256x256, 1 spp, depth 4, no env")
 
 
-def bunny_c2(width=1920, height=1080, spp=4, nu=264, nv=132, env=True) -> SceneConfig:
+def bunny_c2(width=1920, height=1080, spp=4, nu=264, nv=132, env=True, bvh_tracer=None) -> SceneConfig:
     """C2: Cornell box + ~70k-triangle bunny stand-in + vignaioli_night_1k env."""
     sb = H.SceneBuilder()
     m = H.Material(baseColor=(0.65, 0.65, 0.65))
@@ -88,7 +91,7 @@ def bunny_c2(width=1920, height=1080, spp=4, nu=264, nv=132, env=True) -> SceneC
     rgb = tab = None
     if env:
         rgb, tab = _env_1k()
-    return SceneConfig("C2-bunny", sb.build(), _cornell_camera(width, height), width, height, spp,
+    return SceneConfig("C2-bunny", sb.build(bvh_tracer), _cornell_camera(width, height), width, height, spp,
                        env_rgb=rgb, env_table=tab,
                        description=f"Cornell + bunny stand-in ({nu * nv * 2} tris) + 1k HDR env, "
                                    f"{width}x{height}, {spp} spp")
@@ -115,7 +118,7 @@ def checker_texture(w: int, h: int, ch: int = 3, seed: int = 7):
     return (px.reshape(-1), w, h, ch)
 
 
-def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144) -> SceneConfig:
+def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144, bvh_tracer=None) -> SceneConfig:
     """C3: CornellBox() with its commented-out "marry" model (main.cpp:209) -- a
     UV-mapped ~50k-triangle figure stand-in textured with MC003_Kozakura_Mari.png
     (RGBA 2048x1024, texture unit 5) -- plus SceneFlat()'s metal boards
@@ -135,13 +138,13 @@ def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144) -> SceneConfig:
                              H.scale(0.012, 1.0, 0.004)], bm, f"board{k + 1}", texture_ids=[1])
     rgb, tab = _env_1k()
     tex = [load_texture(MARI_PNG), checker_texture(333, 97, 3)]
-    return SceneConfig("C3-marry", sb.build(), _cornell_camera(width, height), width, height, spp,
+    return SceneConfig("C3-marry", sb.build(bvh_tracer), _cornell_camera(width, height), width, height, spp,
                        env_rgb=rgb, env_table=tab, textures=tex,
                        description=f"Cornell + textured figure stand-in ({nu * nv * 2} tris, Mari 2048x1024 RGBA) "
                                    f"+ metal boards (RGB 333x97) + 1k env")
 
 
-def teapot_c4(width=1920, height=1080, spp=4) -> SceneConfig:
+def teapot_c4(width=1920, height=1080, spp=4, bvh_tracer=None) -> SceneConfig:
     """C4: teapot() scene (main.cpp:329-347) + an emissive quad and the 1k env,
     so the light, environment and BSDF pdfs are all active."""
     sb = H.SceneBuilder()
@@ -154,11 +157,11 @@ def teapot_c4(width=1920, height=1080, spp=4) -> SceneConfig:
                  light, "area_light")
     rgb, tab = _env_1k()
     cam = H.camera_update((0, 5, 5), (0, 0, 0), (0, 1, 0), 45.0, np.float32(width) / np.float32(height))
-    return SceneConfig("C4-teapot", sb.build(), cam, width, height, spp, env_rgb=rgb, env_table=tab,
+    return SceneConfig("C4-teapot", sb.build(bvh_tracer), cam, width, height, spp, env_rgb=rgb, env_table=tab,
                        description="teapot stand-in + floor + area light + 1k env")
 
 
-def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, env_h=2048) -> SceneConfig:
+def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, env_h=2048, bvh_tracer=None) -> SceneConfig:
     """C5: 4,194,304-triangle displaced sphere in the Cornell box, 4k synthetic env."""
     sb = H.SceneBuilder()
     m = H.Material(baseColor=(0.65, 0.65, 0.65))
@@ -167,7 +170,7 @@ def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, e
     _cornell_walls(sb, m)
     rgb = H.synthetic_hdr(env_w, env_h, 0x5EED)
     tab = H.hdr_table(rgb)
-    return SceneConfig("C5-synthetic4m", sb.build(), _cornell_camera(width, height), width, height, spp,
+    return SceneConfig("C5-synthetic4m", sb.build(bvh_tracer), _cornell_camera(width, height), width, height, spp,
                        env_rgb=rgb, env_table=tab,
                        description=f"{nu * nv * 2}-tri displaced sphere + {env_w}x{env_h} synthetic env")
 

@@ -84,6 +84,19 @@ class PathTracer:
         self._ck(self._lib.pnrt_read_env_table(self._ctx, N.fptr(out)), "pnrt_read_env_table")
         return out
 
+    def build_bvh(self, tri_bounds: np.ndarray):
+        """GPU BuildBVH (pnrt_bvh_build): (nodes (nn, 12) float32, order (n,) int32, max_depth)
+        from per-triangle Bound + boundCenter (n, 9) -- the host build's result, bit for bit."""
+        tb = np.ascontiguousarray(tri_bounds, np.float32).reshape(-1, 9)
+        n = len(tb)
+        cap = max(2 * n - 1, 1)
+        nodes = np.empty((cap, 12), np.float32)
+        order = np.empty(n, np.int32)
+        nn, md = ctypes.c_int(), ctypes.c_int()
+        self._ck(self._lib.pnrt_bvh_build(self._ctx, N.fptr(tb), n, N.fptr(nodes), cap, ctypes.byref(nn), N.iptr(order),
+                                          ctypes.byref(md)), "pnrt_bvh_build")
+        return nodes[:nn.value].copy(), order, md.value
+
     def set_frame(self, width: int, height: int, camera: np.ndarray, max_depth: int = 4):
         cam = N.Camera()
         c = np.asarray(camera, np.float32).reshape(4, 3)
