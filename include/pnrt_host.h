@@ -11,7 +11,9 @@
  *                                              pnrt_bvh_build + pnrt_scene_set_bvh)
  *   light prefix list (main.cpp:374-383)       pnrt_scene_build
  *   packing loops (main.cpp:409-524)           pnrt_scene_pack
- *   Camera::UpdateCamera (camera.hpp:11-31)    pnrt_camera_update
+ *   Camera::UpdateCamera (camera.hpp:11-31)    pnrt_camera_update, pnrt_camera_state_init
+ *   Camera::UpdateRotate/TranslateUV/Fov       pnrt_camera_rotate/_translate/_zoom
+ *     (camera.hpp:33-65, main.cpp:118-142)
  *   glm::translate/rotate/scale (main.cpp:207-237)  pnrt_model_matrix
  *   stbi_loadf RGBE (stb_image.h:6839-6990)    pnrt_hdr_decode_rgbe
  *   LoadHDRImage CDF table (shader.hpp:145-203) pnrt_hdr_build_table
@@ -88,6 +90,25 @@ int pnrt_scene_pack(const pnrt_scene* s, float* vertices, float* materials,
 /* camera.hpp:11-31 -> eye, lowerLeftCorner, horizontal, vertical */
 int pnrt_camera_update(const float eye[3], const float center[3], const float up[3],
                        float fov_deg, float aspect, float out12[12]);
+
+/* Camera state (camera.hpp:4-77) and the interactive controls that
+ * main.cpp's mouse callbacks call (main.cpp:118-142): left drag ->
+ * UpdateRotate(dx, dy), right drag -> UpdateTranslateUV(-dx, dy), scroll ->
+ * UpdateFov(yoffset).  eye/lower_left/horizontal/vertical feed pnrt_set_frame.
+ * rotate/zoom return 1 if applied, 0 if the reference rejects the move
+ * (rotation within 0.9995 of the up axis; fov outside (1, 89)). */
+typedef struct {
+    float eye[3], center[3], up[3];
+    float fov_deg, aspect;
+    float u[3], v[3], w[3];
+    float distance;
+    float lower_left[3], horizontal[3], vertical[3];
+} pnrt_camera_state;
+int pnrt_camera_state_init(pnrt_camera_state* c, const float eye[3], const float center[3], const float up[3],
+                           float fov_deg, float aspect);
+int pnrt_camera_rotate(pnrt_camera_state* c, float phi, float theta);
+int pnrt_camera_translate(pnrt_camera_state* c, float dx, float dy);
+int pnrt_camera_zoom(pnrt_camera_state* c, float delta);
 
 /* Radiance RGBE decode with stbi_loadf semantics (3 channels, row 0 = first
  * scanline).  out_rgb may be NULL to query w/h; caller allocates w*h*3. */

@@ -524,6 +524,68 @@ int pnrt_camera_update(const float e[3], const float c[3], const float up_[3], f
     return 0;
 }
 
+// ---- Camera (camera.hpp:4-77): state + the interactive controls main.cpp's
+// mouse callbacks drive (main.cpp:118-142): left drag UpdateRotate, right drag
+// UpdateTranslateUV, scroll UpdateFov.  glm-exact float arithmetic.
+static void cam_update(pnrt_camera_state* c, vec3 eye, vec3 center, vec3 up, float fov, float aspect) {
+    auto put = [](float* d, vec3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
+    put(c->eye, eye); put(c->center, center); put(c->up, up);
+    c->fov_deg = fov;
+    c->aspect = aspect;
+    const float theta = radians(fov);
+    const float halfHeight = (float)std::tan((double)theta * 0.5);   // glm::tan(theta * 0.5): double
+    const float halfWidth = aspect * halfHeight;
+    c->distance = length(eye - center);                               // glm::distance
+    const vec3 w = normalize(eye - center);
+    const vec3 u = normalize(cross(up, w));
+    const vec3 v = cross(w, u);
+    put(c->w, w); put(c->u, u); put(c->v, v);
+    put(c->lower_left, ((eye - halfWidth * u) - halfHeight * v) - w);
+    put(c->horizontal, (2 * halfWidth) * u);
+    put(c->vertical, (2 * halfHeight) * v);
+}
+static vec3 v3(const float* a) { return vec3(a[0], a[1], a[2]); }
+
+extern "C" int pnrt_camera_state_init(pnrt_camera_state* c, const float eye[3], const float center[3],
+                                      const float up[3], float fov, float aspect) {
+    if (!c || !eye || !center || !up) return fail(-1, "camera_state_init: null");
+    cam_update(c, v3(eye), v3(center), v3(up), fov, aspect);
+    return 0;
+}
+
+extern "C" int pnrt_camera_rotate(pnrt_camera_state* c, float phi, float theta) {
+    if (!c) return fail(-1, "camera_rotate: null");
+    phi *= 0.6;                          // float *= double (camera.hpp:34-35)
+    theta *= 0.6;
+    phi = radians(phi);
+    theta = radians(theta);
+    vec3 nv(std::cos(phi) * std::cos(theta), std::sin(phi) * std::cos(theta), std::sin(theta));
+    nv = (v3(c->w) * nv.x + v3(c->u) * nv.y) + v3(c->v) * nv.z;
+    if (std::abs(dot(v3(c->up), nv)) > 0.9995f) return 0;    // rejected: too close to the up axis
+    const vec3 eye = v3(c->center) + nv * c->distance;
+    cam_update(c, eye, v3(c->center), v3(c->up), c->fov_deg, c->aspect);
+    return 1;
+}
+
+extern "C" int pnrt_camera_translate(pnrt_camera_state* c, float dx, float dy) {
+    if (!c) return fail(-1, "camera_translate: null");
+    dx *= 0.05;                          // camera.hpp:47-48
+    dy *= 0.05;
+    const vec3 u = v3(c->u), v = v3(c->v);
+    const vec3 eye = v3(c->eye) + (dx * u + dy * v);
+    const vec3 center = v3(c->center) + (dx * u + dy * v);
+    cam_update(c, eye, center, v3(c->up), c->fov_deg, c->aspect);
+    return 1;
+}
+
+extern "C" int pnrt_camera_zoom(pnrt_camera_state* c, float delta) {
+    if (!c) return fail(-1, "camera_zoom: null");
+    const float nFov = c->fov_deg + delta;   // camera.hpp:57-63
+    if (!(nFov < 89.f && nFov > 1.f)) return 0;
+    cam_update(c, v3(c->eye), v3(c->center), v3(c->up), nFov, c->aspect);
+    return 1;
+}
+
 // ---- Radiance RGBE (stbi_loadf semantics, stb_image.h v2.27 HDR loader) ----------
 int pnrt_hdr_decode_rgbe(const uint8_t* bytes, int64_t n, int* pw, int* ph, float* out) {
     if (!bytes || !pw || !ph) return fail(-1, "rgbe: null");
