@@ -190,7 +190,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
-    const size_t per_path = 16 * 9 + 4 + 4 + 2 + 96 + 1;  // S0-3,S5, C0-3 | flags | hit | occ | 3 ray records | counts
+    const size_t per_path = 16 * 7 + 4 + 4 + 2 + 96 + 1;   // P0-P6 | flags | hit | occ | 3 ray records | counts
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
@@ -208,7 +208,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         WfBufs b;
         size_t n = (size_t)tiles_x * tiles_y * 64 * cf;
         char* base = static_cast<char*>(c->wf);
-        float4** f4[] = {&b.S0, &b.S1, &b.S2, &b.S3, &b.S5, &b.C0, &b.C1, &b.C2, &b.C3};
+        float4** f4[] = {&b.P0, &b.P1, &b.P2, &b.P3, &b.P4, &b.P5, &b.P6};
         size_t off = 0;
         for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
         b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
@@ -257,7 +257,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
             {
                 ProfScope ps(c, PNRT_K_SHADE);
                 // MIS + continuation, then the next bounce's sampling
-                hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, c->stream, s, fp, b, c->colors);
+                hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, c->stream, s, fp, b, (const float4*)c->primary,
+                                   c->colors);
             }
             HIPCHK(c, hipGetLastError());
         }

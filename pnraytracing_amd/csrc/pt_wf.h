@@ -19,7 +19,7 @@
 #define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
 #endif
 #ifndef WF_REFILL_PCT
-#define WF_REFILL_PCT 50    // refill a wave when at most this % of its lanes still trace
+#define WF_REFILL_PCT 65    // refill a wave when at most this % of its lanes still trace
 #endif
 #define WF_OVF 56
 #define WF_TRACE_BLOCK 256
@@ -33,18 +33,16 @@
 #define WF_RCONT 8u
 
 struct WfBufs {
-    // path state
-    float4* S0;   // P.xyz, u
-    float4* S1;   // N.xyz, v
-    float4* S2;   // Lo.xyz, bits(mat | (tex+1)<<24)
-    float4* S3;   // cw.xyz, bits(seed)
-    float4* S5;   // base.xyz, -
-    uint32_t* flags;
-    // bounce candidates
-    float4* C0;   // LDirect.xyz, lightPDF
-    float4* C1;   // LEnvironment.xyz, enPDF
-    float4* C2;   // dBRDF.xyz, |N.L|
-    float4* C3;   // L.xyz, dPDF
+    // path state between setup and shade: exactly what shade reads, 112 B per
+    // path (the primary hit's base colour is re-read from the primary record)
+    float4* P0;   // continuation origin (P + N*1e-4).xyz, dPDF
+    float4* P1;   // L.xyz, |N.L|
+    float4* P2;   // dBRDF.xyz, -
+    float4* P3;   // LDirect.xyz, lightPDF      (candidate, if the light ray is unoccluded)
+    float4* P4;   // LEnvironment.xyz, enPDF    (candidate, if the env ray is unoccluded)
+    float4* P5;   // Lo.xyz, bits(seed)
+    float4* P6;   // throughput.xyz, -
+    uint32_t* flags;   // dense: paths that end are cleared with coalesced 4-B stores
     // trace results
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
@@ -79,6 +77,9 @@ PN_DEV void wf_coords(const WfBufs& b, uint32_t s, int& x, int& lr, int& k) {
     lr = ty * 8 + (p >> 3);
 }
 
+// a path slot that ends (or never starts) is marked dead
+PN_DEV void wf_kill(const WfBufs& b, uint32_t i) { b.flags[i] = 0u; }
+
 PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
     color = mk3(clampf(color.x, 0.f, 1.f), clampf(color.y, 0.f, 1.f), clampf(color.z, 0.f, 1.f));
     colors[((size_t)k * fp.rows + lr) * fp.width + x] = make_float4(color.x, color.y, color.z, 0.f);
@@ -87,7 +88,7 @@ PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr,
 // Path state a bounce's setup starts from (in registers: the fused kernels
 // hand it over without a round trip through HBM).
 struct PathIn {
-    f3 P, N, V, cw;
+    f3 P, N, V, cw, Lo;
     float u, v;
     int mt;            // material | (texture + 1) << 24
     uint32_t seed;
@@ -102,7 +103,7 @@ struct BounceRays {
 };
 
 // Returns the path's flags for the bounce (alive, bounce, which rays exist);
-// writes the bounce candidates C0-C3, S3 and flags; the rays go to `rays`.
+// writes the path state P0-P6; the rays go to `rays`.
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, int bounce,
                               int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const f3 P = q.P, N = q.N, V = q.V;
@@ -148,6 +149,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         rays.dL = ldir;
         nfl |= WF_RLIGHT;
     }
+    b.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);     // stored as soon as final: shorter live ranges
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -162,6 +164,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
+    b.P4[i] = make_float4(LE.x, LE.y, LE.z, pe);
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -207,15 +210,15 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     float dPDF = (pDiffuse * pdfDiffuse + pSpecular * pdfSpecular) + pClearcoat * pdfClearcoat;
     f3 dBRDF = disney(bc, L);
     float NdotL = pnm_fabs(dot(N, L));
-    b.C0[i] = make_float4(LD.x, LD.y, LD.z, pl);
-    b.C1[i] = make_float4(LE.x, LE.y, LE.z, pe);
-    b.C2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, NdotL);
-    b.C3[i] = make_float4(L.x, L.y, L.z, dPDF);
-    b.S3[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(seed));
-    b.flags[i] = nfl | WF_RCONT;
     rays.dC = L;
     rays.oP = P;
     rays.oOff = add(P, muls(N, 0.0001f));
+    b.P0[i] = make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF);
+    b.P1[i] = make_float4(L.x, L.y, L.z, NdotL);
+    b.P2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, 0.f);
+    b.flags[i] = nfl | WF_RCONT;
+    b.P5[i] = make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed));
+    b.P6[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, 0.f);
     return nfl | WF_RCONT;
 }
 
@@ -262,8 +265,12 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
     }
 }
 
+#ifndef WF_SHADE_WAVES
+#define WF_SHADE_WAVES 4      // waves per SIMD for the gen/shade kernels (<= 128 VGPRs)
+#endif
+
 // ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
-__global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
+__global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
                                                        float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t nfl = 0;
@@ -271,7 +278,7 @@ __global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams f
     if (i < b.n) {
         int x, lr, k;
         wf_coords(b, i, x, lr, k);
-        b.flags[i] = 0;
+        wf_kill(b, i);
         if (x < fp.width && lr < fp.rows) {
             const float4* rec = primary + 3 * ((size_t)lr * fp.width + x);
             const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
@@ -289,11 +296,8 @@ __global__ void __launch_bounds__(256) pt_wf_gen_setup(DevScene s, FrameParams f
                 q.u = q1.w; q.v = q2.x; q.mt = mt;
                 q.V = neg(camera_dir(fp, x, py));
                 q.cw = mk3(1.f, 1.f, 1.f);
+                q.Lo = mk3(0.f, 0.f, 0.f);
                 q.seed = ((uint32_t)x * 1973u + (uint32_t)py * 9277u + frame * 26699u) | 1u;
-                b.S0[i] = make_float4(q.P.x, q.P.y, q.P.z, q.u);
-                b.S1[i] = make_float4(q.N.x, q.N.y, q.N.z, q.v);
-                b.S2[i] = make_float4(0.f, 0.f, 0.f, __int_as_float(mt));
-                b.S5[i] = make_float4(base.x, base.y, base.z, 0.f);
                 nfl = wf_setup_core(s, fp, b, i, 0, x, py, frame, q, rays);
             }
         }
@@ -546,20 +550,19 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 }
 
 // ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
-PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, float4* colors, uint32_t i,
-                              BounceRays& rays) {
+PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, const float4* primary,
+                              float4* colors, uint32_t i, BounceRays& rays) {
     const uint32_t fl = b.flags[i];
     if (!(fl & WF_ALIVE)) return 0;
     int bounce = (int)((fl >> 8) & 7u);
-    float4 c0 = b.C0[i], c1 = b.C1[i], c2 = b.C2[i], c3 = b.C3[i];
-    float4 s2 = b.S2[i], s3 = b.S3[i];
-    f3 LD = mk3(c0.x, c0.y, c0.z), LE = mk3(c1.x, c1.y, c1.z);
-    float pl = c0.w, pe = c1.w;
+    const float4 p0 = b.P0[i], p1 = b.P1[i], p2 = b.P2[i], p3 = b.P3[i], p4 = b.P4[i], p5 = b.P5[i], p6 = b.P6[i];
+    f3 LD = mk3(p3.x, p3.y, p3.z), LE = mk3(p4.x, p4.y, p4.z);
+    float pl = p3.w, pe = p4.w;
     if ((fl & WF_RLIGHT) && b.occ[2 * (size_t)i]) { LD = mk3(0.f, 0.f, 0.f); pl = 0.f; }     // :890
     if (!(fl & WF_RENV) || b.occ[2 * (size_t)i + 1]) LE = mk3(0.f, 0.f, 0.f);                 // :922
-    f3 dBRDF = mk3(c2.x, c2.y, c2.z), L = mk3(c3.x, c3.y, c3.z);
-    float NdotL = c2.w, dPDF = c3.w;
-    f3 Lo = mk3(s2.x, s2.y, s2.z), cw = mk3(s3.x, s3.y, s3.z);
+    f3 dBRDF = mk3(p2.x, p2.y, p2.z), L = mk3(p1.x, p1.y, p1.z);
+    float NdotL = p1.w, dPDF = p0.w;
+    f3 Lo = mk3(p5.x, p5.y, p5.z), cw = mk3(p6.x, p6.y, p6.z);
     float invPDFSum = 1.0f / ((pe + pl) + dPDF);
     f3 mis = add(muls(LE, pe), muls(LD, pl));
     Lo = add(Lo, muls(mul(cw, mis), invPDFSum));
@@ -571,42 +574,38 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
             f3 enLi = env_color(s, normalize(L));
             Lo = add(Lo, divs(muls(mul(mul(cw, enLi), dBRDF), NdotL), dPDF));
         }
-        float4 s5 = b.S5[i];
-        wf_write_color(fp, colors, k, lr, x, add(mk3(s5.x, s5.y, s5.z), Lo));
-        b.flags[i] = 0;
+        const float4 q2 = primary[3 * ((size_t)lr * fp.width + x) + 2];     // the primary hit's base colour
+        wf_write_color(fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
+        wf_kill(b, i);
         return 0;
     }
-    float4 s0 = b.S0[i], s1 = b.S1[i];
-    f3 P = mk3(s0.x, s0.y, s0.z), N = mk3(s1.x, s1.y, s1.z);
-    RayP r = make_ray(add(P, muls(N, 0.0001f)), L, 0);
+    RayP r = make_ray(mk3(p0.x, p0.y, p0.z), L, 0);        // the continuation ray as traced
     Hit h = make_hit(s, r, ht);
     f3 em = get_emissive(s, h.mat);
     Lo = add(Lo, divs(muls(mul(mul(cw, em), dBRDF), NdotL), dPDF));
     cw = mul(cw, divs(muls(dBRDF, NdotL), dPDF));
     ++bounce;
     if (bounce >= fp.max_depth) {
-        float4 s5 = b.S5[i];
-        wf_write_color(fp, colors, k, lr, x, add(mk3(s5.x, s5.y, s5.z), Lo));
-        b.flags[i] = 0;
+        const float4 q2 = primary[3 * ((size_t)lr * fp.width + x) + 2];
+        wf_write_color(fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
+        wf_kill(b, i);
         return 0;
     }
     // the next bounce starts here: its setup runs on the state in registers
-    const int mt = (h.mat & 0x00ffffff) | ((h.tex + 1) << 24);
-    b.S0[i] = make_float4(h.P.x, h.P.y, h.P.z, h.u);
-    b.S1[i] = make_float4(h.N.x, h.N.y, h.N.z, h.v);
-    b.S2[i] = make_float4(Lo.x, Lo.y, Lo.z, __int_as_float(mt));
     PathIn q;
-    q.P = h.P; q.N = h.N; q.u = h.u; q.v = h.v; q.mt = mt;
-    q.V = neg(L); q.cw = cw; q.seed = __float_as_uint(s3.w);
+    q.P = h.P; q.N = h.N; q.u = h.u; q.v = h.v;
+    q.mt = (h.mat & 0x00ffffff) | ((h.tex + 1) << 24);
+    q.V = neg(L); q.cw = cw; q.Lo = Lo; q.seed = __float_as_uint(p5.w);
     const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
     return wf_setup_core(s, fp, b, i, bounce, x, py, b.first_frame + (uint32_t)k, q, rays);
 }
 
 // ---- shade + next-bounce setup: MIS, continuation hit (:936-972), then the next
 // bounce's sampling for the paths that continue ----------------------------------------------
-__global__ void __launch_bounds__(256) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b, float4* colors) {
+__global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
+                                                         float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     BounceRays rays;
-    const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, colors, i, rays) : 0u;
+    const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, primary, colors, i, rays) : 0u;
     wf_enqueue(b, i, nfl, rays);     // every lane of the wave reaches this point
 }
