@@ -130,13 +130,15 @@ def main():
     image = None
 
     def step(k):
-        nonlocal image
         sf.render(spp * k, spp)
         if world > 1:
-            image = sf.gather()                # one RCCL gather of the row bands to rank 0
+            sf.gather_async()                  # one RCCL gather of the row bands to rank 0, overlapped
+                                               # with the next step's rendering
 
     for k in range(args.warmup):
         step(k)
+    if world > 1:
+        sf.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -147,6 +149,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k)
+    if world > 1:
+        image = sf.finish()                    # every gather completes inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -47,11 +47,18 @@ class ShardedFrame:
         self.rows = [torch.as_tensor(r, device=self.device) for r in rows]
         self.my_rows = len(rows[self.rank])
         self.max_rows = max(len(r) for r in rows)           # rank 0 owns the most (first bands)
-        # equal-sized buffers for the collective; the tail of a short shard is padding
-        self.send = torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=self.device)
+        # equal-sized buffers for the collective; the tail of a short shard is padding.
+        # Two slots, so the gather of step k runs on the RCCL stream while step k+1
+        # renders (gather_async / finish)
         cdev = torch.device("cpu") if self.stage else self.device
-        self.recv = [torch.zeros(self.send.shape, dtype=torch.float32, device=cdev) for _ in range(self.world)] \
-            if self.rank == 0 else None
+        self.sendb = [torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=self.device) for _ in range(2)]
+        self.recvb = [[torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=cdev) for _ in range(self.world)]
+                      if self.rank == 0 else None for _ in range(2)]
+        self.send, self.recv = self.sendb[0], self.recvb[0]
+        self._slot = 0
+        self._work = [None, None]
+        self._last = None
+        self._newest = 0
         self.image = torch.zeros((H, W, 4), dtype=torch.float32, device=self.device) if self.rank == 0 else None
         if self.device.type == "cuda" and hasattr(tracer, "set_stream"):
             tracer.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
@@ -72,11 +79,43 @@ class ShardedFrame:
         dist.gather(send, self.recv if self.rank == 0 else None, dst=0, group=self.group)
         if self.rank != 0:
             return None
+        return self._assemble(self.recv)
+
+    def _assemble(self, recv) -> torch.Tensor:
         for r in range(self.world):
             n = len(self.rows[r])
             if n:
-                self.image.index_copy_(0, self.rows[r], self.recv[r][:n].to(self.device, non_blocking=False))
+                self.image.index_copy_(0, self.rows[r], recv[r][:n].to(self.device, non_blocking=False))
         return self.image
+
+    def gather_async(self) -> None:
+        """Pack this rank's rows and START the gather (RCCL) without making the
+        render stream wait for it: the next frames render while the rows travel
+        over xGMI.  Double-buffered; :meth:`finish` completes the last gather and
+        assembles the image on rank 0.  (Synchronous for one rank / gloo staging.)"""
+        if self.world == 1 or self.stage:
+            self._last = self.gather()
+            return
+        slot = self._slot
+        self._slot ^= 1
+        if self._work[slot] is not None:       # this slot's previous gather must be done before
+            self._work[slot].wait()            # its send buffer is repacked (stream-ordered wait)
+            self._work[slot] = None
+        if self.my_rows:
+            self.tracer.pack_rows(self.sendb[slot].data_ptr(), self.band, self.world, self.rank)
+        self._work[slot] = dist.gather(self.sendb[slot], self.recvb[slot] if self.rank == 0 else None, dst=0,
+                                       group=self.group, async_op=True)
+        self._newest = slot
+
+    def finish(self) -> torch.Tensor | None:
+        """Complete the outstanding gathers; rank 0 gets the newest frame's image."""
+        if self.world == 1 or self.stage:
+            return self._last
+        for slot in (self._newest ^ 1, self._newest):
+            if self._work[slot] is not None:
+                self._work[slot].wait()
+                self._work[slot] = None
+        return self._assemble(self.recvb[self._newest]) if self.rank == 0 else None
 
 
 def row_owner(height: int, band: int, world: int) -> np.ndarray:

@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, w, h, band, frames, out_path):
+def _worker(rank, world, port, w, h, band, frames, out_path, overlap=False):
     sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "oracle")); sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_tracer import OracleTracer
     from pnraytracing_amd import scenes as S
@@ -29,9 +29,15 @@ def _worker(rank, world, port, w, h, band, frames, out_path):
     try:
         tr = OracleTracer(S.cornell_c1(w, h))
         sf = ShardedFrame(tr, band=band, device="cpu")
-        for f0, n in frames:
-            sf.render(f0, n)
-        img = sf.gather()
+        if overlap:                 # bench.py's per-step pattern: render, start the gather, ...
+            for f0, n in frames:
+                sf.render(f0, n)
+                sf.gather_async()
+            img = sf.finish()
+        else:
+            for f0, n in frames:
+                sf.render(f0, n)
+            img = sf.gather()
         # ranks render only their own rows
         from pnraytracing_amd.dist import row_owner
         mine = row_owner(h, band, world) == rank
@@ -44,13 +50,14 @@ def _worker(rank, world, port, w, h, band, frames, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,w,h,band", [(2, 40, 44, 8), (3, 24, 20, 4)])
-def test_gather_equals_single_process(tmp_path, world, w, h, band):
+@pytest.mark.parametrize("world,w,h,band,overlap", [(2, 40, 44, 8, False), (3, 24, 20, 4, False), (2, 40, 44, 8, True),
+                                                   (3, 24, 20, 4, True)])
+def test_gather_equals_single_process(tmp_path, world, w, h, band, overlap):
     import pyoracle
     from pnraytracing_amd import scenes as S
-    frames = [(0, 1), (1, 2)]
+    frames = [(0, 1), (1, 2), (3, 1)]
     out = str(tmp_path / "img.npy")
-    mp.start_processes(_worker, args=(world, _free_port(), w, h, band, frames, out), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), w, h, band, frames, out, overlap), nprocs=world,
                        join=True, start_method="spawn")
     got = np.load(out)
     o = pyoracle.Oracle(S.cornell_c1(w, h))
