@@ -446,6 +446,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         std::memcpy(&nodes[4 * k + 3], meta, 16);
     }
     uint32_t root_ref = childref(0);
+    const int has_leaf_table = leaf_table.empty() ? 0 : 1;
     if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
     // trace-kernel stack bound: at most one deferred sibling per BVH level
     c->wf_stack_need = maxd + 2;
@@ -467,6 +468,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     const float* root = N;
     for (int k = 0; k < 3; ++k) { s.root_min[k] = root[k]; s.root_max[k] = root[3 + k]; }
     s.root_ref = root_ref;
+    s.has_leaf_table = has_leaf_table;
     c->root_is_leaf = fint(root[7]) == -1;
     c->n_interior = (int)order.size();
     c->max_depth = maxd;

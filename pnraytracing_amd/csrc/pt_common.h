@@ -48,6 +48,7 @@ struct DevScene {
     float lights_sum_area;
     float root_min[3], root_max[3];
     uint32_t root_ref;
+    int has_leaf_table;         // some leaf range needed the table (REF_TABLE refs exist)
     int has_hdr, hdr_w, hdr_h;
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad

@@ -88,14 +88,17 @@ PN_DEV bool tri_test(const RayP& r, const float4& t0, const float4& t1, const fl
     float e0 = P1x * P2y - P1y * P2x;
     float e1 = P2x * P0y - P2y * P0x;
     float e2 = P0x * P1y - P0y * P1x;
-    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
-    float det = (e0 + e1) + e2;
-    if (det == 0) return false;
-    float tScaled = (e0 * P0z + e1 * P1z) + e2 * P2z;
-    if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
-    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    // the reference's early-outs (:300-318) as one branch-free predicate: the
+    // arithmetic has no side effects, so evaluating it for rejected triangles
+    // changes nothing, and every comparison keeps its NaN semantics
+    const float det = (e0 + e1) + e2;
+    const float tScaled = (e0 * P0z + e1 * P1z) + e2 * P2z;
+    const float tmd = tMax * det;
+    const bool mixed = ((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0));
+    const bool rejPos = (det > 0) & ((tScaled <= 0) | (tScaled > tmd));
+    const bool rejNeg = (det < 0) & ((tScaled >= 0) | (tScaled < tmd));
     e0o = e0; e1o = e1; e2o = e2; deto = det; tso = tScaled;
-    return true;
+    return !(mixed | (det == 0) | rejPos | rejNeg);
 }
 
 PN_DEV void decode_leaf(const DevScene& s, uint32_t ref, int& start, int& cnt) {

@@ -315,6 +315,20 @@ PN_DEV uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Leaf ref -> triangle range; the leaf-table lookup is behind a scene-uniform
+// (scalar) branch, so scenes without table leaves pay no divergent branch.
+PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& cnt) {
+    start = (int)((ref >> 7) & 0x7fffffu);
+    cnt = (int)(ref & 0x7fu);
+    if (s.has_leaf_table) {
+        if ((ref & (REF_LEAF | REF_TABLE)) == (REF_LEAF | REF_TABLE) && ref != REF_NONE) {
+            const int2 e = s.leaf_table[ref & 0x3fffffffu];
+            start = e.x;
+            cnt = e.y;
+        }
+    }
+}
+
 template <int STK>
 PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, float z) {
     uint2 e = make_uint2(ref, __float_as_uint(z));
@@ -357,7 +371,7 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     float lo = zn < zf ? zn : zf, hi = zn < zf ? zf : zn;
     zlo = lo;
     // zhi <= 0: the whole box is behind the ray in the triangle test's frame
-    return (t1 >= t0) && !(r.cull_ok() && hi <= 0.0f);
+    return (t1 >= t0) & !(r.cull_ok() & (hi <= 0.0f));
 }
 
 #ifndef WF_DIAG_NOSTORE
@@ -478,57 +492,60 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     st[4] += __popcll(__ballot(busy != 0 && lc <= 0 && cur == REF_NONE));
                 }
                 if (busy) {
-                    bool done = false;
+                    // One step, written branch-light: the triangle test and the node
+                    // visit are both evaluated (a wave almost always holds lanes of
+                    // both kinds, so both paths ran anyway) and their results are
+                    // selected per lane; only memory side effects (stack push/pop,
+                    // the result store) and the rare IEEE division stay in branches.
                     const bool isTri = lc > 0;
-                    // ---- the step's single fetch: a triangle record or a node
-                    float4 q0, q1, q2, q3;
-                    if (isTri || cur != REF_NONE) {
-                        const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)cur;
-                        q0 = base[0]; q1 = base[1]; q2 = base[2];
-                        if (!WF_Q3_COND) q3 = base[3];
-                    }
-                    if (WF_Q3_COND && !isTri && cur != REF_NONE) q3 = s.nodes[4 * (size_t)cur + 3];
-                    if (isTri) {
-                        float e0, e1, e2, det, ts;
-                        if (tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts)) {
-                            hitTri = lt;
-                            if (any) done = true;
-                            else tMax = ts * (1.0f / det);
-                        }
-                        ++lt; --lc;
-                    } else if (cur != REF_NONE) {
-                        const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y),
-                                                   __float_as_uint(q3.z), __float_as_uint(q3.w));
-                        const float tmc = tMax * 1.000001f;
-                        float zloL, zloR;
-                        bool hL = box_fast<ID>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
-                        bool hR = box_fast<ID>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
-                        if (r.cull_ok()) {
-                            if (zloL > tmc && zloL > 1e-20f) hL = false;
-                            if (zloR > tmc && zloR > 1e-20f) hR = false;
-                        }
-                        bool rightFirst = comp(r.d, (int)m.z) < 0;     // :448
-                        uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
-                        bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
-                        float zFar = rightFirst ? zloL : zloR;
-                        if (hNear && hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
-                        uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
-                        if (go != REF_NONE && (go & REF_LEAF)) { decode_leaf(s, go, lt, lc); go = REF_NONE; }
-                        cur = go;
-                    }
+                    const bool isNode = !isTri & (cur != REF_NONE);
+                    // ---- the step's single fetch: a triangle record or a node (lanes
+                    // with neither re-read node 0, which stays in L1)
+                    const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)(isNode ? cur : 0u);
+                    const float4 q0 = base[0], q1 = base[1], q2 = base[2], q3 = base[3];
+                    // triangle test (:254-357 / :360-424)
+                    float e0, e1, e2, det, ts;
+                    const bool acc = tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts) & isTri;
+                    hitTri = acc ? lt : hitTri;
+                    bool done = acc & any;
+                    if (acc & !any) tMax = ts * (1.0f / det);
+                    lt += isTri ? 1 : 0;
+                    lc -= isTri ? 1 : 0;
+                    // node visit: both child boxes (:447-457), z-slab culling
+                    const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
+                                               __float_as_uint(q3.w));
+                    const float tmc = tMax * 1.000001f;
+                    float zloL, zloR;
+                    bool hL = box_fast<ID>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+                    bool hR = box_fast<ID>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
+                    const bool cull = r.cull_ok();
+                    hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
+                    hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
+                    const bool rightFirst = comp(r.d, (int)(m.z & 3u)) < 0;     // :448
+                    const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+                    const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+                    const float zFar = rightFirst ? zloL : zloR;
+                    if (hNear & hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
+                    const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
+                    const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
+                    int gs, gc;
+                    decode_leaf_fast(s, go, gs, gc);
+                    lt = goLeaf ? gs : lt;
+                    lc = goLeaf ? gc : lc;
+                    cur = isNode ? (goLeaf ? REF_NONE : go) : cur;
                     // ---- next fetch target: pop when nothing is pending
-                    if (!done && lc <= 0 && cur == REF_NONE) {
-                        if (sp == 0) {
-                            done = true;
-                        } else {
-                            uint2 e = wf_pop<STK>(lds, wf_ovf(b, tl), tl, sp);
-                            float z = __uint_as_float(e.y);
-                            bool culled = r.cull_ok() && z > tMax * 1.000001f && z > 1e-20f;
-                            if (!culled) {
-                                if (e.x & REF_LEAF) decode_leaf(s, e.x, lt, lc);
-                                else cur = e.x;
-                            }
-                        }
+                    const bool idle = !done & (lc <= 0) & (cur == REF_NONE);
+                    done = done | (idle & (sp == 0));
+                    if (idle & (sp > 0)) {
+                        const uint2 e = wf_pop<STK>(lds, wf_ovf(b, tl), tl, sp);
+                        const float z = __uint_as_float(e.y);
+                        const bool culled = cull & (z > tMax * 1.000001f) & (z > 1e-20f);
+                        const bool eLeaf = (e.x & REF_LEAF) != 0u;
+                        int es, ec;
+                        decode_leaf_fast(s, e.x, es, ec);
+                        lt = (!culled & eLeaf) ? es : lt;
+                        lc = (!culled & eLeaf) ? ec : lc;
+                        cur = (!culled & !eLeaf) ? e.x : cur;
                     }
                     if (done) {
                         const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
