@@ -48,7 +48,7 @@ class SceneConfig:
         return len(self.packed.triangles)
 
 
-def _cornell_walls(sb: H.SceneBuilder, m: H.Material, floor_mat: H.Material | None = None):
+def _cornell_walls(sb: H.SceneBuilder, m: H.Material, floor_mat: H.Material | None = None, light: bool = True):
     """CornellBox() walls (main.cpp:204-237): floor.obj x6 with the reference transforms."""
     q = H.mesh_quad(27.5)
     fm = floor_mat or m
@@ -60,6 +60,8 @@ def _cornell_walls(sb: H.SceneBuilder, m: H.Material, floor_mat: H.Material | No
     sb.add_model(q, [H.translate(-2.75, 2.75, 0.0), H.rotate(-90.0, 0, 0, 1), H.scale(0.1)], m, "left_wall")
     m = m.copy(baseColor=(0.73, 0.73, 0.73))
     sb.add_model(q, [H.translate(0, 5.54, 0), H.rotate(180.0, 0, 0, 1), H.scale(0.1)], m, "ceiling")
+    if not light:
+        return
     m = m.copy(emssive=(60.0, 60.0, 60.0))
     sb.add_model(q, [H.translate(0, 5.54, 0), H.rotate(180.0, 0, 0, 1), H.scale(0.02)], m, "ceiling_light")
 
