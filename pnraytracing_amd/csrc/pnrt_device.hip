@@ -469,6 +469,13 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     for (int k = 0; k < 3; ++k) { s.root_min[k] = root[k]; s.root_max[k] = root[3 + k]; }
     s.root_ref = root_ref;
     s.has_leaf_table = has_leaf_table;
+    {   // GetLightIndex is a lower bound: a linear scan returns the same index iff the
+        // prefix areas are non-decreasing (they are for main.cpp:374-383's list)
+        bool mono = nl <= WF_LIGHT_SCAN;
+        for (int k = 1; mono && k < nl; ++k) mono = lights[k].y >= lights[k - 1].y;
+        for (int k = 0; mono && k < nl; ++k) mono = lights[k].y == lights[k].y;
+        s.light_scan = mono ? 1 : 0;
+    }
     c->root_is_leaf = fint(root[7]) == -1;
     c->n_interior = (int)order.size();
     c->max_depth = maxd;

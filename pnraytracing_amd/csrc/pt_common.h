@@ -49,6 +49,7 @@ struct DevScene {
     float root_min[3], root_max[3];
     uint32_t root_ref;
     int has_leaf_table;         // some leaf range needed the table (REF_TABLE refs exist)
+    int light_scan;             // <= WF_LIGHT_SCAN lights with non-decreasing prefix areas
     int has_hdr, hdr_w, hdr_h;
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad

@@ -52,22 +52,70 @@ PN_DEV int wrap_repeat(float fl, int n) {
     if (i < 0) i += n;
     return i;
 }
-PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
+// A bilinear lookup split into its fetch (the four texels) and its weighting,
+// so callers can put independent fetches in flight before using the result;
+// sample = taps_resolve(taps_fetch(...)) is the one-piece lookup.
+struct Taps4 {
+    float4 t00, t10, t01, t11;
+    float a, b;
+};
+PN_DEV Taps4 taps_clamp(const float4* img, int w, int h, float u, float v) {
+    Taps4 t;
     float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
     float flu = floorf(fu), flv = floorf(fv);
-    float a = fu - flu, b = fv - flv;
+    t.a = fu - flu; t.b = fv - flv;
     int i0 = wrap_clamp(flu, w), i1 = wrap_clamp(flu + 1.0f, w);
     int j0 = wrap_clamp(flv, h), j1 = wrap_clamp(flv + 1.0f, h);
-    float4 t00 = img[(size_t)j0 * w + i0], t10 = img[(size_t)j0 * w + i1];
-    float4 t01 = img[(size_t)j1 * w + i0], t11 = img[(size_t)j1 * w + i1];
+    t.t00 = img[(size_t)j0 * w + i0]; t.t10 = img[(size_t)j0 * w + i1];
+    t.t01 = img[(size_t)j1 * w + i0]; t.t11 = img[(size_t)j1 * w + i1];
+    return t;
+}
+PN_DEV f3 taps_resolve(const Taps4& t) {
+    const float a = t.a, b = t.b;
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    return mk3(((w00 * t.t00.x + w10 * t.t10.x) + w01 * t.t01.x) + w11 * t.t11.x,
+               ((w00 * t.t00.y + w10 * t.t10.y) + w01 * t.t01.y) + w11 * t.t11.y,
+               ((w00 * t.t00.z + w10 * t.t10.z) + w01 * t.t01.z) + w11 * t.t11.z);
+}
+PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
+    return taps_resolve(taps_clamp(img, w, h, u, v));
+}
+PN_DEV f3 texel_u8(const DevScene& s, uint32_t px) {
+    return mk3(s.unorm8[px & 0xffu], s.unorm8[(px >> 8) & 0xffu], s.unorm8[(px >> 16) & 0xffu]);
+}
+// UNORM8 -> float as GL defines it, c / 255 correctly rounded: the same value as
+// the host-built table, without a dependent table lookup
+PN_DEV float unorm8(uint32_t c) { return (float)c / 255.0f; }
+PN_DEV f3 texel_u8_div(uint32_t px) {
+    return mk3(unorm8(px & 0xffu), unorm8((px >> 8) & 0xffu), unorm8((px >> 16) & 0xffu));
+}
+struct AlbedoTaps {
+    uint32_t t00, t10, t01, t11;
+    float a, b;
+};
+// the fetch half of sample_albedo (t is a bound texture: the caller checked)
+PN_DEV AlbedoTaps albedo_fetch(const DevScene& s, int t, float u, float v) {
+    AlbedoTaps r;
+    int w = s.tex_w[t], h = s.tex_h[t];
+    const uint32_t* img = s.tex[t];
+    float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
+    float flu = floorf(fu), flv = floorf(fv);
+    r.a = fu - flu; r.b = fv - flv;
+    int i0 = wrap_repeat(flu, w), i1 = wrap_repeat(flu + 1.0f, w);
+    int j0 = wrap_repeat(flv, h), j1 = wrap_repeat(flv + 1.0f, h);
+    r.t00 = img[(size_t)j0 * w + i0]; r.t10 = img[(size_t)j0 * w + i1];
+    r.t01 = img[(size_t)j1 * w + i0]; r.t11 = img[(size_t)j1 * w + i1];
+    return r;
+}
+PN_DEV f3 albedo_resolve(const AlbedoTaps& r) {
+    f3 t00 = texel_u8_div(r.t00), t10 = texel_u8_div(r.t10), t01 = texel_u8_div(r.t01), t11 = texel_u8_div(r.t11);
+    const float a = r.a, b = r.b;
     float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
     return mk3(((w00 * t00.x + w10 * t10.x) + w01 * t01.x) + w11 * t11.x,
                ((w00 * t00.y + w10 * t10.y) + w01 * t01.y) + w11 * t11.y,
                ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);
 }
-PN_DEV f3 texel_u8(const DevScene& s, uint32_t px) {
-    return mk3(s.unorm8[px & 0xffu], s.unorm8[(px >> 8) & 0xffu], s.unorm8[(px >> 16) & 0xffu]);
-}
+PN_DEV bool texture_bound(const DevScene& s, int t) { return t >= 0 && t < s.n_tex && s.tex[t] != nullptr; }
 // texture(textures[t], uv).rgb (:871): REPEAT, LINEAR at level 0; unbound -> 0
 PN_DEV f3 sample_albedo(const DevScene& s, int t, float u, float v) {
     if (t < 0 || t >= s.n_tex || s.tex[t] == nullptr) return mk3(0.f, 0.f, 0.f);
@@ -94,6 +142,24 @@ PN_DEV f3 env_color(const DevScene& s, f3 v) {
     u = u + 0.5f; w = w + 0.5f;
     w = 1.0f - w;
     return sample_clamp(s.hdr, s.hdr_w, s.hdr_h, u, w);
+}
+
+// SampleHDRImage (:560-576) in two halves: env_dir turns the RandomHDR taps at
+// (r1, r2) into the direction and pdf and fetches the radiance taps.
+PN_DEV Taps4 env_dir(const DevScene& s, const Taps4& paramTaps, f3& L, float& pdf) {
+    f3 param = taps_resolve(paramTaps);
+    param.y = 1.0f - param.y;
+    float phi = (2.0f * PT_PI) * (param.x - 0.5f);
+    float theta = PT_PI * (param.y - 0.5f);
+    float st, ct, sp, cp;
+    pnm_sincos(theta, st, ct);
+    pnm_sincos(phi, sp, cp);
+    L = mk3(ct * cp, st, ct * sp);
+    pdf = param.z;
+    float sinTheta = fmax_(1e-10f, st);
+    float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
+    pdf = pdf * convert;
+    return taps_clamp(s.hdr, s.hdr_w, s.hdr_h, param.x, param.y);
 }
 
 // SampleHDRImage (:560-576); r1, r2 drawn by the caller in order

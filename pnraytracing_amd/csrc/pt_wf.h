@@ -21,6 +21,9 @@
 #ifndef WF_REFILL_PCT
 #define WF_REFILL_PCT 65    // refill a wave when at most this % of its lanes still trace
 #endif
+#ifndef WF_LIGHT_SCAN
+#define WF_LIGHT_SCAN 8     // light lists up to this long are scanned with all probes in flight
+#endif
 #define WF_OVF 56
 #define WF_TRACE_BLOCK 256
 #define WF_CHUNK 256u        // rays per dequeue
@@ -102,8 +105,45 @@ struct BounceRays {
     f3 dL, dE, dC;
 };
 
+// GetLightIndex (:237-251) as a lower bound over the non-decreasing prefix
+// areas: short lists (s.light_scan, checked monotone at upload) are scanned
+// with every probe in flight at once -- the same index as the binary search.
+PN_DEV int light_index_fast(const DevScene& s, float u) {
+    if (!s.light_scan) return light_index(s, u);
+    const float randomArea = u * s.lights_sum_area;
+    float2 e[WF_LIGHT_SCAN];
+#pragma unroll
+    for (int k = 0; k < WF_LIGHT_SCAN; ++k) e[k] = k < s.n_lights ? s.lights[k] : make_float2(0.f, 0.f);
+    int ans = -1;
+#pragma unroll
+    for (int k = WF_LIGHT_SCAN - 1; k >= 0; --k)
+        if (k < s.n_lights && e[k].y >= randomArea) ans = k;
+    int idx = 0;
+#pragma unroll
+    for (int k = 0; k < WF_LIGHT_SCAN; ++k) idx = (k == ans) ? (int)e[k].x : idx;
+    return idx;                                      // ans < 0 -> 0, as light_index
+}
+
+// The light triangle's records (TriangleSample :598-624, emission :887).
+struct LightFetch {
+    float4 va0, vb0, va1, vb1, va2, vb2;
+    f3 li;
+};
+PN_DEV LightFetch light_fetch(const DevScene& s, int triIndex) {
+    LightFetch f;
+    const int4 id = s.tri_idx[triIndex];
+    const int lmat = __float_as_int(s.tris[3 * (size_t)triIndex + 2].y);
+    f.va0 = s.verts[2 * (size_t)id.x]; f.vb0 = s.verts[2 * (size_t)id.x + 1];
+    f.va1 = s.verts[2 * (size_t)id.y]; f.vb1 = s.verts[2 * (size_t)id.y + 1];
+    f.va2 = s.verts[2 * (size_t)id.z]; f.vb2 = s.verts[2 * (size_t)id.z + 1];
+    f.li = get_emissive(s, lmat);
+    return f;
+}
+
 // Returns the path's flags for the bounce (alive, bounce, which rays exist);
-// writes the path state P0-P6; the rays go to `rays`.
+// writes the path state P0-P6; the rays go to `rays`.  (Issuing the light and
+// environment fetches ahead of the material math was measured: the extra live
+// registers cost a wave per SIMD and more than the overlap gained.)
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, int bounce,
                               int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const f3 P = q.P, N = q.N, V = q.V;
@@ -111,7 +151,10 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     uint32_t seed = q.seed;
 
     Material m = get_material(s, hmat);
-    if (htex != -1) m.baseColor = sample_albedo(s, htex, q.u, q.v);
+    if (htex != -1) {
+        if (texture_bound(s, htex)) m.baseColor = albedo_resolve(albedo_fetch(s, htex, q.u, q.v));
+        else m.baseColor = mk3(0.f, 0.f, 0.f);                                        // unbound unit -> 0
+    }
     f3 T, B;
     if (N.z > 0.9999995f) T = mk3(1.f, 0.f, 0.f);
     else T = normalize(cross(N, mk3(0.f, 0.f, 1.f)));
@@ -122,30 +165,27 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     // direct light (:878-909): candidate values, used if the shadow ray is unoccluded
     f3 LD = mk3(0.f, 0.f, 0.f);
     float pl = 0.f;
-    int triIndex = light_index(s, rand01(seed));
-    if (triIndex != -1) {
+    const float uSel = rand01(seed);
+    if (s.n_lights > 0) {                            // light_index() == -1 iff no lights
+        const LightFetch lf = light_fetch(s, light_index_fast(s, uSel));
         float u0 = rand01(seed), u1 = rand01(seed);
-        int4 id = s.tri_idx[triIndex];
-        float4 va0 = s.verts[2 * (size_t)id.x], vb0 = s.verts[2 * (size_t)id.x + 1];
-        float4 va1 = s.verts[2 * (size_t)id.y], vb1 = s.verts[2 * (size_t)id.y + 1];
-        float4 va2 = s.verts[2 * (size_t)id.z], vb2 = s.verts[2 * (size_t)id.z + 1];
         float su0 = sqrtf(u0);
         float bx = 1.0f - su0, by = u1 * su0, bz = (1.0f - bx) - by;
-        f3 p0 = mk3(va0.x, va0.y, va0.z), p1 = mk3(va1.x, va1.y, va1.z), p2 = mk3(va2.x, va2.y, va2.z);
-        f3 n0 = mk3(va0.w, vb0.x, vb0.y), n1 = mk3(va1.w, vb1.x, vb1.y), n2 = mk3(va2.w, vb2.x, vb2.y);
+        f3 p0 = mk3(lf.va0.x, lf.va0.y, lf.va0.z), p1 = mk3(lf.va1.x, lf.va1.y, lf.va1.z);
+        f3 p2 = mk3(lf.va2.x, lf.va2.y, lf.va2.z);
+        f3 n0 = mk3(lf.va0.w, lf.vb0.x, lf.vb0.y), n1 = mk3(lf.va1.w, lf.vb1.x, lf.vb1.y);
+        f3 n2 = mk3(lf.va2.w, lf.vb2.x, lf.vb2.y);
         f3 lp = add(add(muls(p0, bx), muls(p1, by)), muls(p2, bz));
         f3 ln;
         if (iszero3(n0) || iszero3(n1) || iszero3(n2)) ln = normalize(cross(sub(p1, p0), sub(p2, p0)));
         else ln = add(add(muls(n0, bx), muls(n1, by)), muls(n2, bz));
         ln = normalize(ln);
-        int lmat = __float_as_int(s.tris[3 * (size_t)triIndex + 2].y);
         f3 ldir = sub(lp, P);
         float dis2 = (ldir.x * ldir.x + ldir.y * ldir.y) + ldir.z * ldir.z;
         f3 lightL = normalize(ldir);
         pl = dis2 / (pnm_fabs(dot(ln, neg(lightL))) * s.lights_sum_area);
-        f3 li = get_emissive(s, lmat);
         f3 lightBRDF = disney(bc, lightL);
-        LD = divs(muls(mul(lightBRDF, li), pnm_fabs(dot(N, lightL))), pl);
+        LD = divs(muls(mul(lightBRDF, lf.li), pnm_fabs(dot(N, lightL))), pl);
         rays.dL = ldir;
         nfl |= WF_RLIGHT;
     }
