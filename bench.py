@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-image", default="")
+    ap.add_argument("--spp", type=int, default=0, help="experiment: samples per step other than the config's 4")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     return ap.parse_args()
@@ -116,6 +117,8 @@ def main():
 
     builders = {"C2": scenes.bunny_c2, "C3": scenes.marry_c3, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
     cfg = builders[args.config]()
+    if args.spp:
+        cfg.spp = args.spp
     W, H, spp = cfg.width, cfg.height, cfg.spp
 
     pt = PathTracer(local)

@@ -85,6 +85,11 @@ struct pnrt_ctx {
     float4* colors = nullptr;   size_t colors_cap = 0;
     void* wf = nullptr;         size_t wf_cap = 0;
     uint2* wf_ovf = nullptr;    size_t wf_ovf_cap = 0;
+    uint2* wf_ovf2 = nullptr;   size_t wf_ovf2_cap = 0;
+    // second half of each frame group runs on this stream, concurrently with the
+    // first half on `stream`, so one half's kernels fill the other's trace tail
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int trace_grid = 0;
     int wf_stack_need = 0;                 // wide-traversal stack entries per lane (from upload)
     // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
@@ -113,22 +118,23 @@ static hipEvent_t ev_get(pnrt_ctx* c) {
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
 }
-struct ProfScope {     // records on the context stream, so it times exactly that stream's launches
-    pnrt_ctx* c; int k; hipEvent_t a = nullptr;
-    ProfScope(pnrt_ctx* c_, int k_) : c(c_), k(k_) {
-        if (c->prof_on && (a = ev_get(c))) (void)hipEventRecord(a, c->stream);
+struct ProfScope {     // records on the launch stream, so it times exactly that stream's launches
+    pnrt_ctx* c; int k; hipStream_t st; hipEvent_t a = nullptr;
+    ProfScope(pnrt_ctx* c_, int k_, hipStream_t st_ = nullptr) : c(c_), k(k_), st(st_ ? st_ : c_->stream) {
+        if (c->prof_on && (a = ev_get(c))) (void)hipEventRecord(a, st);
     }
     ~ProfScope() {
         if (!a) return;
         hipEvent_t b = ev_get(c);
         if (!b) { c->ev_pool.push_back(a); return; }
-        (void)hipEventRecord(b, c->stream);
+        (void)hipEventRecord(b, st);
         c->ev_pending.push_back({k, {a, b}});
     }
 };
 static int prof_collect(pnrt_ctx* c) {
     if (c->ev_pending.empty()) return PNRT_OK;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
     for (auto& p : c->ev_pending) {
         float ms = 0.f;
         HIPCHK(c, hipEventElapsedTime(&ms, p.second.first, p.second.second));
@@ -146,6 +152,7 @@ static int prof_collect(pnrt_ctx* c) {
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
     (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
     (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
@@ -175,27 +182,123 @@ static int upload(pnrt_ctx* c, const std::vector<T>& v, const T** out) {
 
 static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 
-// v3 wavefront: primary pass, then per frame chunk gen -> {setup, trace, shade}
-// x max_depth -> ordered blend.
+// Wavefront buffers of one batch of n path slots, carved from `base`.
+static size_t wf_bytes(size_t n) {
+    const size_t npad = (n + 255) / 256 * 256;
+    return n * (16 * 7 + 4 + 4 + 2) + 256 + npad * 96 + (npad / 256) * 12 + 256 + 256 + 512 +
+           (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
+}
+static WfBufs wf_layout(char* base, size_t n) {
+    WfBufs b;
+    float4** f4[] = {&b.P0, &b.P1, &b.P2, &b.P3, &b.P4, &b.P5, &b.P6};
+    size_t off = 0;
+    for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
+    b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
+    b.hit = reinterpret_cast<int*>(base + off); off += n * 4;
+    b.occ = reinterpret_cast<uint8_t*>(base + off); off += n * 2;
+    off = (off + 255) & ~(size_t)255;
+    b.npad = (uint32_t)((n + 255) / 256 * 256);
+    b.nseg_k = b.npad / 256;
+    b.rayO = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
+    b.rayD = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
+    b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
+    off = (off + 255) & ~(size_t)255;
+    b.counter = reinterpret_cast<unsigned int*>(base + off);
+    b.stats = reinterpret_cast<unsigned long long*>(base + off + 64);
+    b.n = (uint32_t)n;
+    return b;
+}
+
+// One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
+// its colours land in frame slots [0, cf) of `colors`.
+static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, WfBufs b, hipStream_t st,
+                        float4* colors) {
+    const dim3 g((unsigned)((b.n + 255) / 256));
+    {   // path state + bounce-0 sampling
+        ProfScope ps(c, PNRT_K_GEN, st);
+        hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, (const float4*)c->primary, colors);
+    }
+    HIPCHK(c, hipGetLastError());
+    for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
+        // segment dequeue counter (+ the WF_STATS census)
+        HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 32, st));
+        {
+            ProfScope ps(c, PNRT_K_TRACE, st);
+            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, st, s, b,
+                               fp.mode);
+        }
+        HIPCHK(c, hipGetLastError());
+        if (WF_TIMING) {   // tail census: when the queue ran dry vs when the last wave ended
+            const size_t nw = (size_t)c->trace_grid * (WF_TRACE_BLOCK / 64);
+            std::vector<unsigned long long> t(4 * nw);
+            HIPCHK(c, hipStreamSynchronize(st));
+            HIPCHK(c, hipMemcpy(t.data(), b.stats + 8, t.size() * 8, hipMemcpyDeviceToHost));
+            unsigned long long t0 = ~0ull, tex = ~0ull, tend = 0;
+            std::vector<unsigned long long> ends;
+            for (size_t w = 0; w < nw; ++w) {
+                t0 = std::min(t0, t[4 * w]);
+                if (t[4 * w + 1]) tex = std::min(tex, t[4 * w + 1]);
+                tend = std::max(tend, t[4 * w + 2]);
+                ends.push_back(t[4 * w + 2]);
+            }
+            std::sort(ends.begin(), ends.end());
+            auto us = [&](unsigned long long v) { return (double)(v - t0) / 100.0; };
+            fprintf(stderr, "[trace timing] bounce %d n=%u first-empty %.1f us, wave ends p10 %.1f p50 %.1f p90 %.1f "
+                    "max %.1f us\n", bounce, b.n, us(tex), us(ends[nw / 10]), us(ends[nw / 2]), us(ends[nw * 9 / 10]),
+                    us(tend));
+        }
+        if (WF_STATS) {
+            unsigned long long stt[8];
+            HIPCHK(c, hipStreamSynchronize(st));
+            HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
+            fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu pop-only=%llu "
+                    "refills=%llu rays=%llu  lane-steps/ray=%.1f\n", bounce, b.n, stt[0],
+                    stt[0] ? (double)stt[1] / stt[0] : 0.0, stt[2], stt[3], stt[4], stt[5], stt[6],
+                    stt[6] ? (double)stt[1] / stt[6] : 0.0);
+        }
+        {
+            ProfScope ps(c, PNRT_K_SHADE, st);
+            // MIS + continuation, then the next bounce's sampling
+            hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, st, s, fp, b, (const float4*)c->primary, colors);
+        }
+        HIPCHK(c, hipGetLastError());
+    }
+    return PNRT_OK;
+}
+
+// v3 wavefront: primary pass, then per group of <= 8 frames: two half-batches
+// on two streams (each gen -> {trace -> shade} x depth), joined, then the
+// frame-ordered blend.  The halves are independent path sets, so running them
+// concurrently changes nothing in the result; it lets one half's kernels fill
+// the CUs the other half's trace kernel leaves idle while its last rays drain.
 static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
     const size_t pix = (size_t)fp.rows * c->width;
     const uint32_t chunk = nf < WF_MAX_CHUNK_FRAMES ? nf : WF_MAX_CHUNK_FRAMES;
     const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
-    const size_t nmax = (size_t)tiles_x * tiles_y * 64 * chunk;
+    const size_t per_frame = (size_t)tiles_x * tiles_y * 64;
     if (c->trace_grid == 0) {
         int per_cu = 0, cus = 0;
         HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false>, WF_TRACE_BLOCK, 0));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
+    const bool split = WF_SPLIT && chunk >= 2;
+    if (split && !c->aux) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
-    const size_t per_path = 16 * 7 + 4 + 4 + 2 + 96 + 1;   // P0-P6 | flags | hit | occ | 3 ray records | counts
+    const size_t ovf_bytes = (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8;
+    const uint32_t cfA0 = split ? (chunk + 1) / 2 : chunk;
+    const size_t bytesA = wf_bytes(per_frame * cfA0), bytesB = split ? wf_bytes(per_frame * (chunk - cfA0)) : 0;
     int rc;
     if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
         (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, &c->wf, &c->wf_cap, (nmax + 256) * per_path + 65536)) ||   // npad rounding + alignment
-        (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8)))
+        (rc = grow(c, &c->wf, &c->wf_cap, bytesA + bytesB + 512)) ||
+        (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, ovf_bytes)) ||
+        (split && (rc = grow(c, (void**)&c->wf_ovf2, &c->wf_ovf2_cap, ovf_bytes))))
         return rc;
     {
         ProfScope ps(c, PNRT_K_PRIMARY);
@@ -204,64 +307,30 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     HIPCHK(c, hipGetLastError());
     for (uint32_t f0 = 0; f0 < nf; f0 += chunk) {
-        uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
-        WfBufs b;
-        size_t n = (size_t)tiles_x * tiles_y * 64 * cf;
+        const uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
+        const uint32_t cfA = split && cf >= 2 ? (cf + 1) / 2 : cf, cfB = cf - cfA;
         char* base = static_cast<char*>(c->wf);
-        float4** f4[] = {&b.P0, &b.P1, &b.P2, &b.P3, &b.P4, &b.P5, &b.P6};
-        size_t off = 0;
-        for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
-        b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
-        b.hit = reinterpret_cast<int*>(base + off); off += n * 4;
-        b.occ = reinterpret_cast<uint8_t*>(base + off); off += n * 2;
-        off = (off + 255) & ~(size_t)255;
-        b.npad = (uint32_t)((n + 255) / 256 * 256);
-        b.nseg_k = b.npad / 256;
-        b.rayO = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
-        b.rayD = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
-        b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
-        off = (off + 255) & ~(size_t)255;
-        off = (off + 255) & ~(size_t)255;
-        b.counter = reinterpret_cast<unsigned int*>(base + off);
-        b.stats = reinterpret_cast<unsigned long long*>(base + off + 64); off += 256;
-        b.ovf = c->wf_ovf;
-        b.ovf_stride = (uint32_t)ovf_stride;
-        b.n = (uint32_t)n;
-        b.chunk_frames = (int)cf;
-        b.tiles_x = tiles_x;
-        b.first_frame = first + f0;
-        const dim3 g((unsigned)((n + 255) / 256));
-        {   // path state + bounce-0 sampling
-            ProfScope ps(c, PNRT_K_GEN);
-            hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, c->stream, s, fp, b, (const float4*)c->primary,
-                               c->colors);
+        WfBufs a = wf_layout(base, per_frame * cfA);
+        a.ovf = c->wf_ovf;
+        a.ovf_stride = (uint32_t)ovf_stride;
+        a.chunk_frames = (int)cfA;
+        a.tiles_x = tiles_x;
+        a.first_frame = first + f0;
+        if (cfB) {
+            WfBufs bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
+            bb.ovf = c->wf_ovf2;
+            bb.ovf_stride = (uint32_t)ovf_stride;
+            bb.chunk_frames = (int)cfB;
+            bb.tiles_x = tiles_x;
+            bb.first_frame = first + f0 + cfA;
+            // the aux stream starts after everything already queued on the main stream
+            HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+            HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+            if ((rc = render_batch(c, s, fp, bb, c->aux, c->colors + (size_t)cfA * pix))) return rc;
+            HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
         }
-        HIPCHK(c, hipGetLastError());
-        for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
-            // segment dequeue counter (+ the WF_STATS census)
-            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 32, c->stream));
-            {
-                ProfScope ps(c, PNRT_K_TRACE);
-                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, c->stream,
-                                   s, b, fp.mode);
-            }
-            HIPCHK(c, hipGetLastError());
-            if (WF_STATS) {
-                unsigned long long st[8];
-                HIPCHK(c, hipStreamSynchronize(c->stream));
-                HIPCHK(c, hipMemcpy(st, b.stats, sizeof st, hipMemcpyDeviceToHost));
-                fprintf(stderr, "[trace stats] bounce %d n=%zu iters=%llu active/iter=%.1f tri=%llu node=%llu pop-only=%llu "
-                        "refills=%llu rays=%llu  lane-steps/ray=%.1f\n", bounce, n, st[0], st[0] ? (double)st[1] / st[0] : 0.0,
-                        st[2], st[3], st[4], st[5], st[6], st[6] ? (double)st[1] / st[6] : 0.0);
-            }
-            {
-                ProfScope ps(c, PNRT_K_SHADE);
-                // MIS + continuation, then the next bounce's sampling
-                hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, c->stream, s, fp, b, (const float4*)c->primary,
-                                   c->colors);
-            }
-            HIPCHK(c, hipGetLastError());
-        }
+        if ((rc = render_batch(c, s, fp, a, c->stream, c->colors))) return rc;
+        if (cfB) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
         {
             ProfScope ps(c, PNRT_K_BLEND);
             hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
@@ -315,7 +384,10 @@ void pnrt_destroy(pnrt_ctx* c) {
     (void)hipFree(c->unorm8);
     (void)hipFree(c->accum);
     (void)hipFree(c->primary); (void)hipFree(c->colors);
-    (void)hipFree(c->wf); (void)hipFree(c->wf_ovf);
+    (void)hipFree(c->wf); (void)hipFree(c->wf_ovf); (void)hipFree(c->wf_ovf2);
+    if (c->aux) { (void)hipStreamSynchronize(c->aux); (void)hipStreamDestroy(c->aux); }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->own_stream);

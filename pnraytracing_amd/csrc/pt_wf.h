@@ -21,6 +21,9 @@
 #ifndef WF_REFILL_PCT
 #define WF_REFILL_PCT 65    // refill a wave when at most this % of its lanes still trace
 #endif
+#ifndef WF_SPLIT
+#define WF_SPLIT 1          // render each frame group as two concurrent half-batches (two streams)
+#endif
 #ifndef WF_LIGHT_SCAN
 #define WF_LIGHT_SCAN 8     // light lists up to this long are scanned with all probes in flight
 #endif
@@ -420,6 +423,12 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
+#ifndef WF_CONT_FIRST
+#define WF_CONT_FIRST 1     // dequeue continuation-ray segments before the shadow-ray segments
+#endif
+#ifndef WF_TIMING
+#define WF_TIMING 0         // diagnostic builds: per-wave timestamps of the trace kernel
+#endif
 #ifndef WF_Q3_COND
 #define WF_Q3_COND 0        // node lanes only fetch the refs/axis quarter (triangle lanes skip it)
 #endif
@@ -458,6 +467,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     // rays are dequeued one queue segment at a time (<= 256 rays of one kind from
     // 256 neighbouring paths, kind-major); one atomic per segment
     const uint32_t nseg = 3u * b.nseg_k;
+    uint64_t t_start = WF_TIMING ? __builtin_amdgcn_s_memrealtime() : 0, t_exh = 0;
+    uint32_t n_rays = 0;
     uint32_t next = 0, end = 0, ckind = 0;
     bool exhausted = false;
 
@@ -479,12 +490,15 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 uint32_t seg = 0;
                 if (lane == 0) seg = atomicAdd(b.counter, 1u);
                 seg = __builtin_amdgcn_readfirstlane(seg);
-                if (seg >= nseg) exhausted = true;
+                if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
                 else {
-                    ckind = seg / b.nseg_k;
-                    const uint32_t j = seg - ckind * b.nseg_k;
+                    // kind order of the sweep: continuation rays (closest hit, the
+                    // longest traversals) first, so the launch ends on short shadow rays
+                    const uint32_t qk = seg / b.nseg_k;
+                    const uint32_t j = seg - qk * b.nseg_k;
+                    ckind = WF_CONT_FIRST ? (qk == 0u ? 2u : qk - 1u) : qk;
                     next = ckind * b.npad + j * 256u;
-                    end = next + b.segcount[seg];
+                    end = next + b.segcount[ckind * b.nseg_k + j];
                 }
             }
             if (idle != 0 && next < end) {
@@ -601,6 +615,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         };
         if (__ballot(busy != 0 && r.kz() != 2) == 0) run(std::true_type{});
         else run(std::false_type{});
+    }
+    if (WF_TIMING && lane == 0) {      // diagnostic builds: per-wave start / queue-empty / end (100 MHz clock)
+        unsigned long long* t = b.stats + 8 + 4 * ((size_t)blockIdx.x * (WF_TRACE_BLOCK / 64) + (threadIdx.x >> 6));
+        t[0] = t_start; t[1] = t_exh; t[2] = __builtin_amdgcn_s_memrealtime(); t[3] = 0;
     }
     if (WF_STATS && lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(b.stats + k, st[k]);
