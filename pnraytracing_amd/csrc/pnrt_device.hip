@@ -185,7 +185,7 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 // Wavefront buffers of one batch of n path slots, carved from `base`.
 static size_t wf_bytes(size_t n) {
     const size_t npad = (n + 255) / 256 * 256;
-    return n * (16 * 7 + 4 + 4 + 2) + 256 + npad * 96 + (npad / 256) * 12 + 256 + 256 + 512 +
+    return n * (16 * 7 + 4 + 4 + 2) + 256 + npad * 96 + (npad / 256) * 12 + 256 + 2048 + 256 + 512 +
            (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
 }
 static WfBufs wf_layout(char* base, size_t n) {
@@ -203,8 +203,8 @@ static WfBufs wf_layout(char* base, size_t n) {
     b.rayD = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
     b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
     off = (off + 255) & ~(size_t)255;
-    b.counter = reinterpret_cast<unsigned int*>(base + off);
-    b.stats = reinterpret_cast<unsigned long long*>(base + off + 64);
+    b.counter = reinterpret_cast<unsigned int*>(base + off);               // 8 counters, 256 B apart
+    b.stats = reinterpret_cast<unsigned long long*>(base + off + 2048);
     b.n = (uint32_t)n;
     return b;
 }
@@ -221,7 +221,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, W
     HIPCHK(c, hipGetLastError());
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
         // segment dequeue counter (+ the WF_STATS census)
-        HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 256 : 32, st));
+        HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 2048 + 256 : 2048, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, st, s, b,

@@ -423,6 +423,16 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
+#ifndef WF_QSHARDS
+#define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
+#endif
+#ifndef WF_QSTRIDE
+#define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
+#endif
+#ifndef WF_SUB
+#define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
+#endif
+#define WF_NSUB (256 / WF_SUB)
 #ifndef WF_CONT_FIRST
 #define WF_CONT_FIRST 1     // dequeue continuation-ray segments before the shadow-ray segments
 #endif
@@ -466,10 +476,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     const int tl = threadIdx.x, lane = tl & 63;
     // rays are dequeued one queue segment at a time (<= 256 rays of one kind from
     // 256 neighbouring paths, kind-major); one atomic per segment
-    const uint32_t nseg = 3u * b.nseg_k;
+    const uint32_t nseg = 3u * b.nseg_k * WF_NSUB;
     uint64_t t_start = WF_TIMING ? __builtin_amdgcn_s_memrealtime() : 0, t_exh = 0;
     uint32_t n_rays = 0;
-    uint32_t next = 0, end = 0, ckind = 0;
+    uint32_t next = 0, end = 0, ckind = 0, qpart = 0;
     bool exhausted = false;
 
     RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
@@ -487,18 +497,34 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         auto refill = [&]() {
             const uint64_t idle = __ballot(busy == 0);
             if (idle != 0 && next >= end && !exhausted) {
-                uint32_t seg = 0;
-                if (lane == 0) seg = atomicAdd(b.counter, 1u);
-                seg = __builtin_amdgcn_readfirstlane(seg);
+                // WF_QSHARDS dequeue counters, item i on counter i % WF_QSHARDS: the
+                // blocks sharing an XCD (blockIdx % 8) start on their own counter and
+                // move on when it runs dry, so the global sweep order is unchanged
+                // while each counter sees 1/WF_QSHARDS of the device-scope atomics
+                uint32_t seg = nseg;
+                for (;;) {
+                    const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
+                    uint32_t t = 0;
+                    if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
+                    t = __builtin_amdgcn_readfirstlane(t);
+                    const uint32_t item = t * WF_QSHARDS + p;
+                    if (item < nseg) { seg = item; break; }
+                    if (++qpart == WF_QSHARDS) break;
+                }
                 if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
                 else {
-                    // kind order of the sweep: continuation rays (closest hit, the
-                    // longest traversals) first, so the launch ends on short shadow rays
-                    const uint32_t qk = seg / b.nseg_k;
-                    const uint32_t j = seg - qk * b.nseg_k;
+                    // one dequeue = WF_SUB rays of a segment (finer grains balance the
+                    // drain at the end of the launch).  Kind order of the sweep:
+                    // continuation rays (closest hit, the longest traversals) first, so
+                    // the launch ends on short shadow rays
+                    const uint32_t sj = seg / WF_NSUB, part = seg - sj * WF_NSUB;
+                    const uint32_t qk = sj / b.nseg_k;
+                    const uint32_t j = sj - qk * b.nseg_k;
                     ckind = WF_CONT_FIRST ? (qk == 0u ? 2u : qk - 1u) : qk;
-                    next = ckind * b.npad + j * 256u;
-                    end = next + b.segcount[ckind * b.nseg_k + j];
+                    const uint32_t cnt = b.segcount[ckind * b.nseg_k + j];
+                    const uint32_t lo = min(part * (uint32_t)WF_SUB, cnt);
+                    next = ckind * b.npad + j * 256u + lo;
+                    end = ckind * b.npad + j * 256u + min(lo + (uint32_t)WF_SUB, cnt);
                 }
             }
             if (idle != 0 && next < end) {
