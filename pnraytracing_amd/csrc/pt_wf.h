@@ -426,6 +426,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_QSHARDS
 #define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
 #endif
+#ifndef WF_QBAND
+#define WF_QBAND 0          // experiment: shard = image band instead of interleaved items
+#endif
 #ifndef WF_QSTRIDE
 #define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
 #endif
@@ -468,7 +471,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 // wave-level decision (ballot) at a reconvergence point: the ray <-> lane
 // refill runs between traversal phases.
 #ifndef WF_TRACE_WAVES
-#define WF_TRACE_WAVES 5      // waves per SIMD requested from the register allocator (98 -> 96 VGPRs)
+#define WF_TRACE_WAVES 6      // waves per SIMD (80 VGPRs; the few spills are the per-ray result addresses)
 #endif
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
@@ -507,8 +510,18 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     uint32_t t = 0;
                     if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
                     t = __builtin_amdgcn_readfirstlane(t);
+#if WF_QBAND
+                    // shard p = image band p (setup blocks [p n/S, (p+1) n/S)), kind-major
+                    const uint32_t lo = p * b.nseg_k / WF_QSHARDS, w = (p + 1) * b.nseg_k / WF_QSHARDS - lo;
+                    if (t < 3u * w * WF_NSUB) {
+                        const uint32_t kq = t / (w * WF_NSUB), r = t - kq * w * WF_NSUB;
+                        seg = (kq * b.nseg_k + lo + r / WF_NSUB) * WF_NSUB + r % WF_NSUB;
+                        break;
+                    }
+#else
                     const uint32_t item = t * WF_QSHARDS + p;
                     if (item < nseg) { seg = item; break; }
+#endif
                     if (++qpart == WF_QSHARDS) break;
                 }
                 if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
