@@ -80,16 +80,26 @@ struct pnrt_ctx {
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
     int kernel = 3;                        // 3 = wavefront (default), 1 = v1 one-lane-per-pixel
-    // wavefront buffers (grown on demand)
-    float4* primary = nullptr;  size_t primary_cap = 0;
-    float4* colors = nullptr;   size_t colors_cap = 0;
-    void* wf = nullptr;         size_t wf_cap = 0;
-    uint2* wf_ovf = nullptr;    size_t wf_ovf_cap = 0;
-    uint2* wf_ovf2 = nullptr;   size_t wf_ovf2_cap = 0;
-    // second half of each frame group runs on this stream, concurrently with the
-    // first half on `stream`, so one half's kernels fill the other's trace tail
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // Pipelined wavefront rendering.  pnrt_render call k uses pipe[k % 2]: its own
+    // worker stream(s) and primary / colour / path buffers, so call k+1 starts
+    // while call k's kernels drain (one call's kernels fill the CUs the other's
+    // trace kernel leaves idle while its last rays drain).  Only the blends are
+    // ordered: they run in call order on the context stream, which therefore
+    // sees each call's finished image.  (Worker streams + the context stream
+    // stay within the 4 hardware queues a process gets: GPU_MAX_HW_QUEUES.)
+    struct Pipe {
+        hipStream_t w[2] = {nullptr, nullptr};
+        hipEvent_t ev_prim = nullptr, ev_join[2] = {nullptr, nullptr}, ev_blend = nullptr;
+        float4* primary = nullptr;  size_t primary_cap = 0;
+        float4* colors = nullptr;   size_t colors_cap = 0;
+        void* wf = nullptr;         size_t wf_cap = 0;
+        uint2* ovf[2] = {nullptr, nullptr};
+        size_t ovf_cap[2] = {0, 0};
+        bool blend_pending = false;  // ev_blend guards the colour buffer's last reader
+    };
+    Pipe pipe[2];
+    bool pipes_ready = false;
+    uint64_t ncall = 0;
     int trace_grid = 0;
     int wf_stack_need = 0;                 // wide-traversal stack entries per lane (from upload)
     // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
@@ -110,6 +120,15 @@ static int set_err(pnrt_ctx* c, int code, const std::string& m) {
         if (e_ != hipSuccess)                                                                     \
             return set_err(ctx, PNRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
     } while (0)
+
+// every stream the context launches on (user-visible stream, blend stream, workers)
+static hipError_t sync_all(pnrt_ctx* c) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    for (auto& P : c->pipe)
+        for (hipStream_t w : P.w)
+            if (e == hipSuccess && w) e = hipStreamSynchronize(w);
+    return e;
+}
 
 // ---- event timing: a start/stop event pair around every launch of a class ----------------
 static hipEvent_t ev_get(pnrt_ctx* c) {
@@ -133,8 +152,7 @@ struct ProfScope {     // records on the launch stream, so it times exactly that
 };
 static int prof_collect(pnrt_ctx* c) {
     if (c->ev_pending.empty()) return PNRT_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->aux) HIPCHK(c, hipStreamSynchronize(c->aux));
+    HIPCHK(c, sync_all(c));
     for (auto& p : c->ev_pending) {
         float ms = 0.f;
         HIPCHK(c, hipEventElapsedTime(&ms, p.second.first, p.second.second));
@@ -151,8 +169,7 @@ static int prof_collect(pnrt_ctx* c) {
 
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
-    (void)hipStreamSynchronize(c->stream);
-    if (c->aux) (void)hipStreamSynchronize(c->aux);
+    (void)sync_all(c);
     (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
@@ -212,11 +229,11 @@ static WfBufs wf_layout(char* base, size_t n) {
 // One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
 // its colours land in frame slots [0, cf) of `colors`.
 static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, WfBufs b, hipStream_t st,
-                        float4* colors) {
+                        const float4* primary, float4* colors) {
     const dim3 g((unsigned)((b.n + 255) / 256));
     {   // path state + bounce-0 sampling
         ProfScope ps(c, PNRT_K_GEN, st);
-        hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, (const float4*)c->primary, colors);
+        hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
     }
     HIPCHK(c, hipGetLastError());
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
@@ -259,19 +276,34 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, W
         {
             ProfScope ps(c, PNRT_K_SHADE, st);
             // MIS + continuation, then the next bounce's sampling
-            hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, st, s, fp, b, (const float4*)c->primary, colors);
+            hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
         }
         HIPCHK(c, hipGetLastError());
     }
     return PNRT_OK;
 }
 
-// v3 wavefront: primary pass, then per group of <= 8 frames: two half-batches
-// on two streams (each gen -> {trace -> shade} x depth), joined, then the
-// frame-ordered blend.  The halves are independent path sets, so running them
-// concurrently changes nothing in the result; it lets one half's kernels fill
-// the CUs the other half's trace kernel leaves idle while its last rays drain.
+static int pipes_init(pnrt_ctx* c) {
+    if (c->pipes_ready) return PNRT_OK;
+    c->pipes_ready = true;
+    for (auto& P : c->pipe) {
+        for (int k = 0; k < (WF_SPLIT ? 2 : 1); ++k) HIPCHK(c, hipStreamCreateWithFlags(&P.w[k], hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&P.ev_prim, hipEventDisableTiming));
+        for (auto& e : P.ev_join) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&P.ev_blend, hipEventDisableTiming));
+    }
+    return PNRT_OK;
+}
+
+// v3 wavefront, one pnrt_render call on pipe[ncall % 2]: primary pass, then per
+// group of <= 8 frames two half-batches (each gen -> {trace -> shade} x depth) on
+// the pipe's two worker streams, then the frame-ordered blend on the blend stream.
+// The halves and consecutive calls are independent path sets, so running them
+// concurrently changes nothing in the result; the blends keep frame order.
 static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
+    int rc;
+    if ((rc = pipes_init(c))) return rc;
+    pnrt_ctx::Pipe& P = c->pipe[c->ncall & 1];
     const size_t pix = (size_t)fp.rows * c->width;
     const uint32_t chunk = nf < WF_MAX_CHUNK_FRAMES ? nf : WF_MAX_CHUNK_FRAMES;
     const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
@@ -283,60 +315,69 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
     const bool split = WF_SPLIT && chunk >= 2;
-    if (split && !c->aux) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    }
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
     const size_t ovf_bytes = (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8;
     const uint32_t cfA0 = split ? (chunk + 1) / 2 : chunk;
     const size_t bytesA = wf_bytes(per_frame * cfA0), bytesB = split ? wf_bytes(per_frame * (chunk - cfA0)) : 0;
-    int rc;
-    if ((rc = grow(c, (void**)&c->primary, &c->primary_cap, pix * 48)) ||
-        (rc = grow(c, (void**)&c->colors, &c->colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, &c->wf, &c->wf_cap, bytesA + bytesB + 512)) ||
-        (rc = grow(c, (void**)&c->wf_ovf, &c->wf_ovf_cap, ovf_bytes)) ||
-        (split && (rc = grow(c, (void**)&c->wf_ovf2, &c->wf_ovf2_cap, ovf_bytes))))
+    if ((rc = grow(c, (void**)&P.primary, &P.primary_cap, pix * 48)) ||
+        (rc = grow(c, (void**)&P.colors, &P.colors_cap, pix * 16 * chunk)) ||
+        (rc = grow(c, &P.wf, &P.wf_cap, bytesA + bytesB + 512)) ||
+        (rc = grow(c, (void**)&P.ovf[0], &P.ovf_cap[0], ovf_bytes)) ||
+        (split && (rc = grow(c, (void**)&P.ovf[1], &P.ovf_cap[1], ovf_bytes))))
         return rc;
+    ++c->ncall;
+    hipStream_t w0 = P.w[0], w1 = P.w[1] ? P.w[1] : P.w[0];
+    // this pipe's buffers were last read by the blend of call ncall - 2
+    if (P.blend_pending) {
+        HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
+        if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));
+    }
     {
-        ProfScope ps(c, PNRT_K_PRIMARY);
-        hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, s, fp,
-                           c->primary);
+        ProfScope ps(c, PNRT_K_PRIMARY, w0);
+        hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
     }
     HIPCHK(c, hipGetLastError());
+    if (w1 != w0) {
+        HIPCHK(c, hipEventRecord(P.ev_prim, w0));
+        HIPCHK(c, hipStreamWaitEvent(w1, P.ev_prim, 0));
+    }
     for (uint32_t f0 = 0; f0 < nf; f0 += chunk) {
         const uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
         const uint32_t cfA = split && cf >= 2 ? (cf + 1) / 2 : cf, cfB = cf - cfA;
-        char* base = static_cast<char*>(c->wf);
+        char* base = static_cast<char*>(P.wf);
         WfBufs a = wf_layout(base, per_frame * cfA);
-        a.ovf = c->wf_ovf;
+        a.ovf = P.ovf[0];
         a.ovf_stride = (uint32_t)ovf_stride;
         a.chunk_frames = (int)cfA;
         a.tiles_x = tiles_x;
         a.first_frame = first + f0;
+        if (f0) {                        // the previous group's blend has read the colours
+            HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
+            if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));
+        }
         if (cfB) {
             WfBufs bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
-            bb.ovf = c->wf_ovf2;
+            bb.ovf = P.ovf[1];
             bb.ovf_stride = (uint32_t)ovf_stride;
             bb.chunk_frames = (int)cfB;
             bb.tiles_x = tiles_x;
             bb.first_frame = first + f0 + cfA;
-            // the aux stream starts after everything already queued on the main stream
-            HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
-            HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-            if ((rc = render_batch(c, s, fp, bb, c->aux, c->colors + (size_t)cfA * pix))) return rc;
-            HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+            if ((rc = render_batch(c, s, fp, bb, w1, P.primary, P.colors + (size_t)cfA * pix))) return rc;
+            HIPCHK(c, hipEventRecord(P.ev_join[1], w1));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[1], 0));
         }
-        if ((rc = render_batch(c, s, fp, a, c->stream, c->colors))) return rc;
-        if (cfB) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-        {
+        if ((rc = render_batch(c, s, fp, a, w0, P.primary, P.colors))) return rc;
+        HIPCHK(c, hipEventRecord(P.ev_join[0], w0));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[0], 0));
+        {   // the blends run in call order on the caller's stream
             ProfScope ps(c, PNRT_K_BLEND);
             hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
-                               (const float4*)c->colors, c->accum, (int)cf, first + f0);
+                               (const float4*)P.colors, c->accum, (int)cf, first + f0);
         }
         HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(P.ev_blend, c->stream));
+        P.blend_pending = true;
     }
     return PNRT_OK;
 }
@@ -357,6 +398,13 @@ int pnrt_create(int device, pnrt_ctx** out) {
         return PNRT_E_HIP;
     }
     c->stream = c->own_stream;
+    // the pipelined renderer's worker streams are created with the context, so
+    // they take hardware queues of their own before the caller creates more streams
+    if (pipes_init(c) != PNRT_OK) {
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return PNRT_E_HIP;
+    }
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_sobolV), kSobolV, sizeof kSobolV) != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;
@@ -377,17 +425,22 @@ int pnrt_create(int device, pnrt_ctx** out) {
 void pnrt_destroy(pnrt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    (void)sync_all(c);
     free_scene(c);
     (void)hipFree(c->hdr); (void)hipFree(c->rnd);
     for (void* t : c->tex) (void)hipFree(t);
     (void)hipFree(c->unorm8);
     (void)hipFree(c->accum);
-    (void)hipFree(c->primary); (void)hipFree(c->colors);
-    (void)hipFree(c->wf); (void)hipFree(c->wf_ovf); (void)hipFree(c->wf_ovf2);
-    if (c->aux) { (void)hipStreamSynchronize(c->aux); (void)hipStreamDestroy(c->aux); }
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    (void)sync_all(c);
+    for (auto& P : c->pipe) {
+        (void)hipFree(P.primary); (void)hipFree(P.colors); (void)hipFree(P.wf);
+        for (uint2* o : P.ovf) (void)hipFree(o);
+        for (hipStream_t w : P.w) if (w) (void)hipStreamDestroy(w);
+        if (P.ev_prim) (void)hipEventDestroy(P.ev_prim);
+        for (hipEvent_t e : P.ev_join) if (e) (void)hipEventDestroy(e);
+        if (P.ev_blend) (void)hipEventDestroy(P.ev_blend);
+    }
+
     for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->own_stream);
@@ -418,7 +471,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     if (!V || !M || !T || !N || nv <= 0 || nm <= 0 || nt <= 0 || nn <= 0 || nl < 0 || (nl > 0 && !Lt))
         return set_err(c, PNRT_E_ARG, "upload_scene: missing or empty arrays");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     free_scene(c);
     c->scene_bytes = 0;
 
@@ -585,7 +638,7 @@ int pnrt_upload_texture(pnrt_ctx* c, int slot, const uint8_t* px, int w, int h, 
 int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int h) {
     if (!c) return PNRT_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     (void)hipFree(c->hdr); (void)hipFree(c->rnd);
     c->hdr = c->rnd = nullptr;
     c->scene.has_hdr = 0;
@@ -609,7 +662,7 @@ int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
     if (!c) return PNRT_E_ARG;
     if (!rgb || w <= 0 || h <= 0) return set_err(c, PNRT_E_ARG, "upload_env_build: bad arguments");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     (void)hipFree(c->hdr); (void)hipFree(c->rnd);
     c->hdr = c->rnd = nullptr;
     c->scene.has_hdr = 0;
@@ -644,7 +697,7 @@ int pnrt_read_env_table(pnrt_ctx* c, float* out) {
     if (!c || !out) return PNRT_E_ARG;
     if (!c->rnd) return set_err(c, PNRT_E_STATE, "read_env_table: no environment");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     const size_t n = (size_t)c->scene.hdr_w * c->scene.hdr_h;
     std::vector<float4> t(n);
     HIPCHK(c, hipMemcpy(t.data(), c->rnd, n * 16, hipMemcpyDeviceToHost));
@@ -658,7 +711,7 @@ int pnrt_set_frame(pnrt_ctx* c, int w, int h, const pnrt_camera* cam, int depth)
         return set_err(c, PNRT_E_ARG, "set_frame: bad arguments (MAX_BOUNCE_DEPTH must be 0..4: 8 Sobol dims)");
     HIPCHK(c, hipSetDevice(c->device));
     if (w != c->width || h != c->height || !c->accum) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, sync_all(c));
         (void)hipFree(c->accum);
         c->accum = nullptr;
         HIPCHK(c, hipMalloc(&c->accum, (size_t)w * h * 16));
@@ -727,7 +780,7 @@ int pnrt_read_accum(pnrt_ctx* c, float* out) {
     if (!c->accum) return set_err(c, PNRT_E_STATE, "read_accum: no frame");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(out, c->accum, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     return PNRT_OK;
 }
 
@@ -768,7 +821,7 @@ int pnrt_pack_rows(pnrt_ctx* c, void* dst, int band, int nsh, int shard) {
 int pnrt_synchronize(pnrt_ctx* c) {
     if (!c) return PNRT_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     return PNRT_OK;
 }
 
@@ -796,7 +849,7 @@ int pnrt_debug_math(pnrt_ctx* c, int fn, const float* a, const float* b, float* 
     else HIPCHK(c, hipMemset(db, 0, bytes));
     hipLaunchKernelGGL(pt_math_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, fn, da, db, dout, n);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, sync_all(c));
     HIPCHK(c, hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
     (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
     return PNRT_OK;

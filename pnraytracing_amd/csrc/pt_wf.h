@@ -22,7 +22,7 @@
 #define WF_REFILL_PCT 65    // refill a wave when at most this % of its lanes still trace
 #endif
 #ifndef WF_SPLIT
-#define WF_SPLIT 1          // render each frame group as two concurrent half-batches (two streams)
+#define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
 #endif
 #ifndef WF_LIGHT_SCAN
 #define WF_LIGHT_SCAN 8     // light lists up to this long are scanned with all probes in flight
