@@ -80,7 +80,7 @@ struct pnrt_ctx {
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
     int kernel = 3;                        // 3 = wavefront (default), 1 = v1 one-lane-per-pixel
-    // Pipelined wavefront rendering.  pnrt_render call k uses pipe[k % 2]: its own
+    // Pipelined wavefront rendering.  pnrt_render call k uses pipe[k % WF_PIPES]: its own
     // worker stream(s) and primary / colour / path buffers, so call k+1 starts
     // while call k's kernels drain (one call's kernels fill the CUs the other's
     // trace kernel leaves idle while its last rays drain).  Only the blends are
@@ -97,7 +97,7 @@ struct pnrt_ctx {
         size_t ovf_cap[2] = {0, 0};
         bool blend_pending = false;  // ev_blend guards the colour buffer's last reader
     };
-    Pipe pipe[2];
+    Pipe pipe[WF_PIPES];
     bool pipes_ready = false;
     uint64_t ncall = 0;
     int trace_grid = 0;
@@ -303,7 +303,7 @@ static int pipes_init(pnrt_ctx* c) {
 static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
     int rc;
     if ((rc = pipes_init(c))) return rc;
-    pnrt_ctx::Pipe& P = c->pipe[c->ncall & 1];
+    pnrt_ctx::Pipe& P = c->pipe[c->ncall % WF_PIPES];
     const size_t pix = (size_t)fp.rows * c->width;
     const uint32_t chunk = nf < WF_MAX_CHUNK_FRAMES ? nf : WF_MAX_CHUNK_FRAMES;
     const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
@@ -328,7 +328,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         return rc;
     ++c->ncall;
     hipStream_t w0 = P.w[0], w1 = P.w[1] ? P.w[1] : P.w[0];
-    // this pipe's buffers were last read by the blend of call ncall - 2
+    // this pipe's buffers were last read by the blend of call ncall - WF_PIPES
     if (P.blend_pending) {
         HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
         if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));

@@ -21,6 +21,9 @@
 #ifndef WF_REFILL_PCT
 #define WF_REFILL_PCT 65    // refill a wave when at most this % of its lanes still trace
 #endif
+#ifndef WF_PIPES
+#define WF_PIPES 3          // pnrt_render calls in flight (buffer sets / worker streams; + the context stream = 4 HW queues)
+#endif
 #ifndef WF_SPLIT
 #define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
 #endif
