@@ -504,6 +504,18 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         verts[2 * (size_t)i] = make_float4(v[0], v[1], v[2], v[3]);
         verts[2 * (size_t)i + 1] = make_float4(v[4], v[5], v[12], v[13]);
     }
+    // per-triangle shading attributes (normals, uvs of its three vertices), so a
+    // hit's attributes are one fetch away from the triangle index instead of two
+    std::vector<float4> tattr((size_t)nt * 4);
+    for (int i = 0; i < nt; ++i) {
+        const float* v0 = V + 15 * (size_t)tidx[i].x;
+        const float* v1 = V + 15 * (size_t)tidx[i].y;
+        const float* v2 = V + 15 * (size_t)tidx[i].z;
+        tattr[4 * (size_t)i + 0] = make_float4(v0[3], v0[4], v0[5], v1[3]);
+        tattr[4 * (size_t)i + 1] = make_float4(v1[4], v1[5], v2[3], v2[4]);
+        tattr[4 * (size_t)i + 2] = make_float4(v2[5], v0[12], v0[13], v1[12]);
+        tattr[4 * (size_t)i + 3] = make_float4(v1[13], v2[12], v2[13], 0.f);
+    }
     // BVH: validate the reference tree (pre-order, left = id + 1) from the root,
     // number interior nodes, and store child boxes in the parent.
     std::vector<int> dn(nn, -1), depth(nn, 0), order;
@@ -575,18 +587,35 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
     // trace-kernel stack bound: at most one deferred sibling per BVH level
     c->wf_stack_need = maxd + 2;
-    std::vector<float2> lights(nl);
+    std::vector<float2> lights(nl > WF_LIGHT_SCAN ? nl : WF_LIGHT_SCAN, make_float2(0.f, 0.f));
     for (int i = 0; i < nl; ++i) {
         lights[i] = make_float2(Lt[3 * (size_t)i], Lt[3 * (size_t)i + 1]);
         int li = fint(Lt[3 * (size_t)i]);
         if (li < 0 || li >= nt) return set_err(c, PNRT_E_SCENE, "light references an out-of-range triangle");
     }
     std::vector<float> mats(M, M + 18 * (size_t)nm);
+    // light records: what TriangleSample (:598-624) and the emission (:887) read for
+    // light entry k -- its triangle's vertex records and material emission -- in one
+    // place; entry nl is triangle 0 (GetLightIndex's fallback index)
+    std::vector<float4> lrec((size_t)(nl + 1) * 7);
+    for (int e = 0; e <= nl; ++e) {
+        const int t = e < nl ? fint(Lt[3 * (size_t)e]) : 0;
+        for (int k = 0; k < 3; ++k) {
+            const int vi = k == 0 ? tidx[t].x : (k == 1 ? tidx[t].y : tidx[t].z);
+            lrec[7 * (size_t)e + 2 * k] = verts[2 * (size_t)vi];
+            lrec[7 * (size_t)e + 2 * k + 1] = verts[2 * (size_t)vi + 1];
+        }
+        const int mat = fint(T[6 * (size_t)t + 3]);
+        const float* em = M + 18 * (size_t)mat;
+        lrec[7 * (size_t)e + 6] = make_float4(em[0], em[1], em[2], 0.f);
+    }
 
     DevScene& s = c->scene;
     int rc;
     if ((rc = upload(c, nodes, &s.nodes)) || (rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tris, &s.tris)) || (rc = upload(c, tidx, &s.tri_idx)) ||
-        (rc = upload(c, verts, &s.verts)) || (rc = upload(c, mats, &s.materials)) || (rc = upload(c, lights, &s.lights)))
+        (rc = upload(c, verts, &s.verts)) || (rc = upload(c, mats, &s.materials)) || (rc = upload(c, lights, &s.lights)) ||
+        (rc = upload(c, tattr, &s.tri_attr)) || (rc = upload(c, lrec, &s.light_rec)) ||
+        (rc = upload(c, std::vector<float4>(1, make_float4(0.f, 0.f, 0.f, 0.f)), &s.zero4)))
         return rc;
     s.n_nodes = (int)order.size(); s.n_tris = nt; s.n_verts = nv; s.n_materials = nm; s.n_lights = nl;
     s.lights_sum_area = lsum;

@@ -43,7 +43,11 @@ struct DevScene {
     const int4* tri_idx;
     const float4* verts;
     const float* materials;     // 18 f / material (reference layout)
-    const float2* lights;       // (index as float, prefixArea) as uploaded
+    const float2* lights;       // (index as float, prefixArea) as uploaded, zero-padded to >= 8 entries
+    const float4* tri_attr;     // 4 float4 / triangle (BVH order): n0 n1 n2 uv0 uv1 uv2 of its vertices
+    const float4* zero4;        // one float4 (0, 0, 0, 0): the load target of lanes that need no data
+    const float4* light_rec;    // 7 float4 / light entry (+1 for triangle 0): its triangle's vertex
+                                // records va0 vb0 va1 vb1 va2 vb2 and (emission, 0)
     int n_nodes, n_tris, n_verts, n_materials, n_lights;
     float lights_sum_area;
     float root_min[3], root_max[3];

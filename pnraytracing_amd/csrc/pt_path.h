@@ -27,22 +27,41 @@ struct Hit {      // Interaction (:60-67) of an accepted triangle
 // Shading data of the accepted triangle (TriangleIntersect :320-355), recomputed
 // from its index: the edge functions do not depend on tMax, so they equal the
 // values computed when the triangle was accepted.
-PN_DEV Hit make_hit(const DevScene& s, const RayP& r, int tri) {
+#ifndef WF_KO_ATTR
+#define WF_KO_ATTR 0    // timing diagnostic: hit attributes without the vertex fetches (wrong images)
+#endif
+// The accepted triangle's records: its 48-B test record (positions, material,
+// texture) and its attribute record (the vertices' normals and uvs, i.e. the
+// values of vertices[tri_idx[tri]], gathered at upload) -- one fetch level.
+struct HitFetch {
+    float4 t0, t1, t2, a0, a1, a2, a3;
+};
+PN_DEV HitFetch hit_fetch(const DevScene& s, int tri) {
+    HitFetch f;
     const float4* t = s.tris + 3 * (size_t)tri;
-    float4 t0 = t[0], t1 = t[1], t2 = t[2];
+    f.t0 = t[0]; f.t1 = t[1]; f.t2 = t[2];
+    if (WF_KO_ATTR) {
+        f.a0 = f.a1 = f.a2 = f.a3 = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        const float4* ta = s.tri_attr + 4 * (size_t)tri;
+        f.a0 = ta[0]; f.a1 = ta[1]; f.a2 = ta[2]; f.a3 = ta[3];
+    }
+    return f;
+}
+// Shading data of the accepted triangle (TriangleIntersect :320-355), recomputed
+// from its records: the edge functions do not depend on tMax, so they equal the
+// values computed when the triangle was accepted.
+PN_DEV Hit hit_resolve(const RayP& r, const HitFetch& f) {
+    const float4 t0 = f.t0, t1 = f.t1, t2 = f.t2, a0 = f.a0, a1 = f.a1, a2 = f.a2, a3 = f.a3;
     float e0, e1, e2, det, ts;
     tri_test(r, t0, t1, t2, 3.402823466e38f, e0, e1, e2, det, ts);
     float invDet = 1.0f / det;
     float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
-    int4 id = s.tri_idx[tri];
-    float4 va0 = s.verts[2 * (size_t)id.x], vb0 = s.verts[2 * (size_t)id.x + 1];
-    float4 va1 = s.verts[2 * (size_t)id.y], vb1 = s.verts[2 * (size_t)id.y + 1];
-    float4 va2 = s.verts[2 * (size_t)id.z], vb2 = s.verts[2 * (size_t)id.z + 1];
     f3 p0 = mk3(t0.x, t0.y, t0.z), p1 = mk3(t0.w, t1.x, t1.y), p2 = mk3(t1.z, t1.w, t2.x);
-    f3 n0 = mk3(va0.w, vb0.x, vb0.y), n1 = mk3(va1.w, vb1.x, vb1.y), n2 = mk3(va2.w, vb2.x, vb2.y);
+    f3 n0 = mk3(a0.x, a0.y, a0.z), n1 = mk3(a0.w, a1.x, a1.y), n2 = mk3(a1.z, a1.w, a2.x);
     Hit h;
-    h.u = (vb0.z * b0 + vb1.z * b1) + vb2.z * b2;
-    h.v = (vb0.w * b0 + vb1.w * b1) + vb2.w * b2;
+    h.u = (a2.y * b0 + a2.w * b1) + a3.y * b2;
+    h.v = (a2.z * b0 + a3.x * b1) + a3.z * b2;
     f3 nHit;
     if (iszero3(n0) || iszero3(n1) || iszero3(n2)) nHit = normalize(cross(sub(p1, p0), sub(p2, p0)));
     else nHit = add(add(muls(n0, b0), muls(n1, b1)), muls(n2, b2));
@@ -53,6 +72,7 @@ PN_DEV Hit make_hit(const DevScene& s, const RayP& r, int tri) {
     h.tex = __float_as_int(t2.z);
     return h;
 }
+PN_DEV Hit make_hit(const DevScene& s, const RayP& r, int tri) { return hit_resolve(r, hit_fetch(s, tri)); }
 
 // GetLightIndex (:237-251)
 PN_DEV int light_index(const DevScene& s, float u) {

@@ -134,9 +134,13 @@ PN_DEV f3 sample_albedo(const DevScene& s, int t, float u, float v) {
                ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);
 }
 
+#ifndef WF_KO_ENV
+#define WF_KO_ENV 0     // timing diagnostic: environment lookups without memory reads (wrong images)
+#endif
 // GetHDRImageColor (:181-193), invAtan = (0.1591, 0.3183) as written
 PN_DEV f3 env_color(const DevScene& s, f3 v) {
     if (!s.has_hdr) return mk3(0.f, 0.f, 0.f);
+    if (WF_KO_ENV) return mk3(v.x * 0.5f, 0.5f, 0.5f);
     float u = pnm_atan2(v.z, v.x), w = pnm_asin(v.y);
     u = u * 0.1591f; w = w * 0.3183f;
     u = u + 0.5f; w = w + 0.5f;
@@ -164,7 +168,7 @@ PN_DEV Taps4 env_dir(const DevScene& s, const Taps4& paramTaps, f3& L, float& pd
 
 // SampleHDRImage (:560-576); r1, r2 drawn by the caller in order
 PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
-    f3 param = sample_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
+    f3 param = WF_KO_ENV ? mk3(r1, r2, 0.5f) : sample_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
     param.y = 1.0f - param.y;
     float phi = (2.0f * PT_PI) * (param.x - 0.5f);
     float theta = PT_PI * (param.y - 0.5f);
@@ -176,6 +180,7 @@ PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
     float sinTheta = fmax_(1e-10f, st);
     float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
     pdf = pdf * convert;
+    if (WF_KO_ENV) return mk3(param.x, param.y, 0.5f);
     return sample_clamp(s.hdr, s.hdr_w, s.hdr_h, param.x, param.y);
 }
 
@@ -216,6 +221,7 @@ struct BrdfCtx {
     float NdotV;
     f3 Cdlin, Cspec0, Csheen;
     float FV, ax, ay, GsV, GrV, alphaDr;
+    float drA2m1, drK;     // GTR1 at alphaDr: a*a - 1 and PI * log(a*a) (constant per bounce)
     float rough, subsurface, metallic, sheen, clearcoat;
 };
 PN_DEV BrdfCtx brdf_prepare(f3 V, f3 N, f3 X, f3 Y, const Material& m) {
@@ -235,9 +241,21 @@ PN_DEV BrdfCtx brdf_prepare(f3 V, f3 N, f3 X, f3 Y, const Material& m) {
     b.GsV = smithG_aniso(b.NdotV, dot(V, X), dot(V, Y), b.ax, b.ay);
     b.GrV = smithG(b.NdotV, 0.25f);
     b.alphaDr = mixf(0.1f, 0.001f, m.clearcoatGloss);
+    {   // gtr1(., alphaDr)'s NdotH-independent part, computed once instead of per call
+        const float a2 = b.alphaDr * b.alphaDr;
+        b.drA2m1 = a2 - 1.0f;
+        b.drK = PT_PI * pnm_log(a2);
+    }
     b.rough = m.roughness; b.subsurface = m.subsurface; b.metallic = m.metallic;
     b.sheen = m.sheen; b.clearcoat = m.clearcoat;
     return b;
+}
+// gtr1(NdotH, b.alphaDr) (:663-668) from the per-bounce constants: the same
+// float operations in the same order, so the same bits as gtr1()
+PN_DEV float gtr1_ctx(const BrdfCtx& b, float NdotH) {
+    if (b.alphaDr >= 1) return 1.0f / PT_PI;
+    float t = 1.0f + (b.drA2m1 * NdotH) * NdotH;
+    return b.drA2m1 / (b.drK * t);
 }
 // DisneyBRDF (:788-849)
 PN_DEV f3 disney(const BrdfCtx& b, f3 L) {
@@ -256,7 +274,7 @@ PN_DEV f3 disney(const BrdfCtx& b, f3 L) {
     f3 Fs = mixv(b.Cspec0, mk3(1.f, 1.f, 1.f), FH);
     float Gs = smithG_aniso(NdotL, dot(L, b.X), dot(L, b.Y), b.ax, b.ay);
     Gs = Gs * b.GsV;
-    float Dr = gtr1(NdotH, b.alphaDr);
+    float Dr = gtr1_ctx(b, NdotH);
     float Fr = mixf(0.04f, 1.0f, FH);
     float Gr = smithG(NdotL, 0.25f) * b.GrV;
     f3 Fsheen = smul(FH * b.sheen, b.Csheen);

@@ -30,6 +30,9 @@
 #ifndef WF_LIGHT_SCAN
 #define WF_LIGHT_SCAN 8     // light lists up to this long are scanned with all probes in flight
 #endif
+#ifndef WF_KO_P34
+#define WF_KO_P34 0         // timing diagnostic: light/env candidates not stored in the path state (wrong images)
+#endif
 #define WF_OVF 56
 #define WF_TRACE_BLOCK 256
 #define WF_CHUNK 256u        // rays per dequeue
@@ -46,11 +49,11 @@ struct WfBufs {
     // path (the primary hit's base colour is re-read from the primary record)
     float4* P0;   // continuation origin (P + N*1e-4).xyz, dPDF
     float4* P1;   // L.xyz, |N.L|
-    float4* P2;   // dBRDF.xyz, -
-    float4* P3;   // LDirect.xyz, lightPDF      (candidate, if the light ray is unoccluded)
-    float4* P4;   // LEnvironment.xyz, enPDF    (candidate, if the env ray is unoccluded)
+    float4* P2;   // dBRDF.xyz, enPDF
+    float4* P3;   // LDirect.xyz, lightPDF  written iff the path has a light ray, read iff it is unoccluded
+    float4* P4;   // LEnvironment.xyz, -    written iff the path has an env ray, read iff it is unoccluded
     float4* P5;   // Lo.xyz, bits(seed)
-    float4* P6;   // throughput.xyz, -
+    float4* P6;   // throughput.xyz, -      written from bounce 1 on (bounce 0: (1, 1, 1))
     uint32_t* flags;   // dense: paths that end are cleared with coalesced 4-B stores
     // trace results
     uint8_t* occ;      // [2 * n]: light, env occluded
@@ -111,38 +114,46 @@ struct BounceRays {
     f3 dL, dE, dC;
 };
 
-// GetLightIndex (:237-251) as a lower bound over the non-decreasing prefix
-// areas: short lists (s.light_scan, checked monotone at upload) are scanned
-// with every probe in flight at once -- the same index as the binary search.
-PN_DEV int light_index_fast(const DevScene& s, float u) {
-    if (!s.light_scan) return light_index(s, u);
+// GetLightIndex (:237-251) as the light ENTRY it selects (the reference then
+// uses entry.x, its triangle): a lower bound over the non-decreasing prefix
+// areas.  Short lists (s.light_scan, checked monotone at upload; the array is
+// zero-padded to WF_LIGHT_SCAN entries) are scanned with every probe in flight
+// at once -- the same entry as the binary search.  No entry (u * sum beyond the
+// last prefix) -> entry n_lights, whose record is triangle 0's, as the
+// reference's fallback index 0.
+PN_DEV int light_entry(const DevScene& s, float u) {
     const float randomArea = u * s.lights_sum_area;
-    float2 e[WF_LIGHT_SCAN];
-#pragma unroll
-    for (int k = 0; k < WF_LIGHT_SCAN; ++k) e[k] = k < s.n_lights ? s.lights[k] : make_float2(0.f, 0.f);
     int ans = -1;
+    if (s.light_scan) {
+        float2 e[WF_LIGHT_SCAN];
 #pragma unroll
-    for (int k = WF_LIGHT_SCAN - 1; k >= 0; --k)
-        if (k < s.n_lights && e[k].y >= randomArea) ans = k;
-    int idx = 0;
+        for (int k = 0; k < WF_LIGHT_SCAN; ++k) e[k] = s.lights[k];
 #pragma unroll
-    for (int k = 0; k < WF_LIGHT_SCAN; ++k) idx = (k == ans) ? (int)e[k].x : idx;
-    return idx;                                      // ans < 0 -> 0, as light_index
+        for (int k = WF_LIGHT_SCAN - 1; k >= 0; --k)
+            if (k < s.n_lights && e[k].y >= randomArea) ans = k;
+    } else {
+        int L = 0, R = s.n_lights - 1;
+        while (L <= R) {
+            int mid = (L + R) >> 1;
+            if (s.lights[mid].y >= randomArea) { ans = mid; R = mid - 1; }
+            else L = mid + 1;
+        }
+    }
+    return ans < 0 ? s.n_lights : ans;
 }
 
-// The light triangle's records (TriangleSample :598-624, emission :887).
+// The light triangle's records (TriangleSample :598-624, emission :887), one
+// fetch from the light entry.
 struct LightFetch {
     float4 va0, vb0, va1, vb1, va2, vb2;
     f3 li;
 };
-PN_DEV LightFetch light_fetch(const DevScene& s, int triIndex) {
+PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
     LightFetch f;
-    const int4 id = s.tri_idx[triIndex];
-    const int lmat = __float_as_int(s.tris[3 * (size_t)triIndex + 2].y);
-    f.va0 = s.verts[2 * (size_t)id.x]; f.vb0 = s.verts[2 * (size_t)id.x + 1];
-    f.va1 = s.verts[2 * (size_t)id.y]; f.vb1 = s.verts[2 * (size_t)id.y + 1];
-    f.va2 = s.verts[2 * (size_t)id.z]; f.vb2 = s.verts[2 * (size_t)id.z + 1];
-    f.li = get_emissive(s, lmat);
+    const float4* r = s.light_rec + 7 * (size_t)entry;
+    f.va0 = r[0]; f.vb0 = r[1]; f.va1 = r[2]; f.vb1 = r[3]; f.va2 = r[4]; f.vb2 = r[5];
+    const float4 em = r[6];
+    f.li = mk3(em.x, em.y, em.z);
     return f;
 }
 
@@ -173,7 +184,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     float pl = 0.f;
     const float uSel = rand01(seed);
     if (s.n_lights > 0) {                            // light_index() == -1 iff no lights
-        const LightFetch lf = light_fetch(s, light_index_fast(s, uSel));
+        const LightFetch lf = light_fetch(s, light_entry(s, uSel));
         float u0 = rand01(seed), u1 = rand01(seed);
         float su0 = sqrtf(u0);
         float bx = 1.0f - su0, by = u1 * su0, bz = (1.0f - bx) - by;
@@ -195,7 +206,10 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         rays.dL = ldir;
         nfl |= WF_RLIGHT;
     }
-    b.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);     // stored as soon as final: shorter live ranges
+    // stored as soon as final (shorter live ranges), and only when shade can use it:
+    // shade takes (0, 0) for a path without a light ray, as the reference's
+    // initial LDirect / lightPDF (:878-879)
+    if (!WF_KO_P34 && (nfl & WF_RLIGHT)) b.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -210,7 +224,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
-    b.P4[i] = make_float4(LE.x, LE.y, LE.z, pe);
+    if (!WF_KO_P34 && (nfl & WF_RENV)) b.P4[i] = make_float4(LE.x, LE.y, LE.z, 0.f);
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -252,7 +266,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     float LdotH = dot(L, H), NdotH = dot(N, H), NdotLs = dot(N, L);
     float pdfDiffuse = NdotLs * PT_INVPI;
     float pdfSpecular = (gtr2(NdotH, alphaGTR2) * NdotH) / (4.0f * LdotH);
-    float pdfClearcoat = (gtr1(NdotH, alphaGTR1) * NdotH) / (4.0f * LdotH);
+    float pdfClearcoat = (gtr1_ctx(bc, NdotH) * NdotH) / (4.0f * LdotH);
     float dPDF = (pDiffuse * pdfDiffuse + pSpecular * pdfSpecular) + pClearcoat * pdfClearcoat;
     f3 dBRDF = disney(bc, L);
     float NdotL = pnm_fabs(dot(N, L));
@@ -261,10 +275,10 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     rays.oOff = add(P, muls(N, 0.0001f));
     b.P0[i] = make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF);
     b.P1[i] = make_float4(L.x, L.y, L.z, NdotL);
-    b.P2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, 0.f);
+    b.P2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe);
     b.flags[i] = nfl | WF_RCONT;
     b.P5[i] = make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed));
-    b.P6[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, 0.f);
+    if (bounce > 0) b.P6[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, 0.f);
     return nfl | WF_RCONT;
 }
 
@@ -672,18 +686,35 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
     const uint32_t fl = b.flags[i];
     if (!(fl & WF_ALIVE)) return 0;
     int bounce = (int)((fl >> 8) & 7u);
-    const float4 p0 = b.P0[i], p1 = b.P1[i], p2 = b.P2[i], p3 = b.P3[i], p4 = b.P4[i], p5 = b.P5[i], p6 = b.P6[i];
+    const float4 p0 = b.P0[i], p1 = b.P1[i], p2 = b.P2[i], p5 = b.P5[i];
+    const float4 p6 = bounce > 0 ? b.P6[i] : make_float4(1.f, 1.f, 1.f, 0.f);   // bounce 0: throughput (1, 1, 1)
+    const int ht = b.hit[i];
+    // the light / env candidates are read only where they count: an occluded
+    // light ray zeroes LDirect and lightPDF (:890), an occluded or absent env ray
+    // zeroes LEnvironment (:922; enPDF is kept, in P2.w).  Lanes that need neither
+    // read the scene's zero float4 instead (no branch: both loads issue together).
+    const uint32_t oc = reinterpret_cast<const uint16_t*>(b.occ)[i];      // both bytes in one load
+    asm volatile("" ::: "memory");     // keep the hit load in this first batch (the scheduler sinks it)
+    const bool useL = (fl & WF_RLIGHT) && !(oc & 0xffu);
+    const bool useE = (fl & WF_RENV) && !(oc >> 8);
+    float4 p3, p4;
+    if (WF_KO_P34) { p3 = make_float4(p2.x, 0.f, 0.f, 1.f); p4 = make_float4(p2.y, 0.f, 0.f, 1.f); }
+    else {
+        p3 = *(useL ? b.P3 + i : s.zero4);
+        p4 = *(useE ? b.P4 + i : s.zero4);
+    }
+    // the continuation hit's records, in flight while the MIS sum waits for P3/P4
+    // (a miss reads triangle 0's, unused)
+    const HitFetch hf = hit_fetch(s, ht < 0 ? 0 : ht);
+    asm volatile("" ::: "memory");     // issue them here (the scheduler would sink them past the MIS wait)
     f3 LD = mk3(p3.x, p3.y, p3.z), LE = mk3(p4.x, p4.y, p4.z);
-    float pl = p3.w, pe = p4.w;
-    if ((fl & WF_RLIGHT) && b.occ[2 * (size_t)i]) { LD = mk3(0.f, 0.f, 0.f); pl = 0.f; }     // :890
-    if (!(fl & WF_RENV) || b.occ[2 * (size_t)i + 1]) LE = mk3(0.f, 0.f, 0.f);                 // :922
+    float pl = p3.w, pe = p2.w;
     f3 dBRDF = mk3(p2.x, p2.y, p2.z), L = mk3(p1.x, p1.y, p1.z);
     float NdotL = p1.w, dPDF = p0.w;
     f3 Lo = mk3(p5.x, p5.y, p5.z), cw = mk3(p6.x, p6.y, p6.z);
     float invPDFSum = 1.0f / ((pe + pl) + dPDF);
     f3 mis = add(muls(LE, pe), muls(LD, pl));
     Lo = add(Lo, muls(mul(cw, mis), invPDFSum));
-    int ht = b.hit[i];
     int x, lr, k;
     wf_coords(b, i, x, lr, k);
     if (ht < 0) {
@@ -697,7 +728,7 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
         return 0;
     }
     RayP r = make_ray(mk3(p0.x, p0.y, p0.z), L, 0);        // the continuation ray as traced
-    Hit h = make_hit(s, r, ht);
+    Hit h = hit_resolve(r, hf);
     f3 em = get_emissive(s, h.mat);
     Lo = add(Lo, divs(muls(mul(mul(cw, em), dBRDF), NdotL), dPDF));
     cw = mul(cw, divs(muls(dBRDF, NdotL), dPDF));
