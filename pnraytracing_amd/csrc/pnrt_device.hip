@@ -629,6 +629,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         for (int k = 1; mono && k < nl; ++k) mono = lights[k].y >= lights[k - 1].y;
         for (int k = 0; mono && k < nl; ++k) mono = lights[k].y == lights[k].y;
         s.light_scan = mono ? 1 : 0;
+        for (int k = 0; k < WF_LIGHT_SCAN; ++k) s.lscan[k] = k < nl ? lights[k].y : 0.f;
     }
     c->root_is_leaf = fint(root[7]) == -1;
     c->n_interior = (int)order.size();

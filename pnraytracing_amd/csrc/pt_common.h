@@ -17,6 +17,7 @@
 #define PT_SHADOW_EPS 0.0001f
 
 #define PT_MAX_TEXTURES 20
+#define PT_LIGHT_SCAN 8      // light lists up to this long are scanned with all probes at once
 #define PT_STACK 64          // pending far children per lane (host checks depth)
 
 // ---- device scene layout (built from the reference arrays at upload) ----------------
@@ -53,7 +54,8 @@ struct DevScene {
     float root_min[3], root_max[3];
     uint32_t root_ref;
     int has_leaf_table;         // some leaf range needed the table (REF_TABLE refs exist)
-    int light_scan;             // <= WF_LIGHT_SCAN lights with non-decreasing prefix areas
+    int light_scan;             // <= PT_LIGHT_SCAN lights with non-decreasing prefix areas
+    float lscan[PT_LIGHT_SCAN]; // their prefix areas, passed by value: scalar (kernel-argument) loads
     int has_hdr, hdr_w, hdr_h;
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad

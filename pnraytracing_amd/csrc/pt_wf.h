@@ -27,9 +27,7 @@
 #ifndef WF_SPLIT
 #define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
 #endif
-#ifndef WF_LIGHT_SCAN
-#define WF_LIGHT_SCAN 8     // light lists up to this long are scanned with all probes in flight
-#endif
+#define WF_LIGHT_SCAN PT_LIGHT_SCAN
 #ifndef WF_KO_P34
 #define WF_KO_P34 0         // timing diagnostic: light/env candidates not stored in the path state (wrong images)
 #endif
@@ -116,21 +114,18 @@ struct BounceRays {
 
 // GetLightIndex (:237-251) as the light ENTRY it selects (the reference then
 // uses entry.x, its triangle): a lower bound over the non-decreasing prefix
-// areas.  Short lists (s.light_scan, checked monotone at upload; the array is
-// zero-padded to WF_LIGHT_SCAN entries) are scanned with every probe in flight
-// at once -- the same entry as the binary search.  No entry (u * sum beyond the
-// last prefix) -> entry n_lights, whose record is triangle 0's, as the
-// reference's fallback index 0.
+// areas.  Short lists (s.light_scan, checked monotone at upload) are scanned
+// from the kernel arguments (s.lscan: scalar registers, no memory round trip)
+// -- the same entry as the binary search.  No entry (u * sum beyond the last
+// prefix) -> entry n_lights, whose record is triangle 0's, as the reference's
+// fallback index 0.
 PN_DEV int light_entry(const DevScene& s, float u) {
     const float randomArea = u * s.lights_sum_area;
     int ans = -1;
     if (s.light_scan) {
-        float2 e[WF_LIGHT_SCAN];
-#pragma unroll
-        for (int k = 0; k < WF_LIGHT_SCAN; ++k) e[k] = s.lights[k];
 #pragma unroll
         for (int k = WF_LIGHT_SCAN - 1; k >= 0; --k)
-            if (k < s.n_lights && e[k].y >= randomArea) ans = k;
+            if (k < s.n_lights && s.lscan[k] >= randomArea) ans = k;
     } else {
         int L = 0, R = s.n_lights - 1;
         while (L <= R) {
@@ -157,17 +152,34 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
     return f;
 }
 
+#ifndef WF_EARLY
+#define WF_EARLY 1          // 1: light record fetched with the material, 2: + the env table taps
+#endif
 // Returns the path's flags for the bounce (alive, bounce, which rays exist);
-// writes the path state P0-P6; the rays go to `rays`.  (Issuing the light and
-// environment fetches ahead of the material math was measured: the extra live
-// registers cost a wave per SIMD and more than the overlap gained.)
+// writes the path state P0-P6; the rays go to `rays`.
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, int bounce,
                               int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const f3 P = q.P, N = q.N, V = q.V;
     const int hmat = q.mt & 0x00ffffff, htex = (int)((uint32_t)q.mt >> 24) - 1;
     uint32_t seed = q.seed;
-
+    // the bounce's light and environment draws (:880, :884, :918) come first in the
+    // stream and depend on nothing else, so they are drawn up front (same order)
+    const float uSel = rand01(seed);
+    float u0 = 0.f, u1 = 0.f, r1 = 0.f, r2 = 0.f;
+    if (s.n_lights > 0) { u0 = rand01(seed); u1 = rand01(seed); }
+    if (s.has_hdr) { r1 = rand01(seed); r2 = rand01(seed); }
+#if WF_EARLY >= 1
+    // light record (and env table taps) in flight with the material fetch
+    const LightFetch lf = light_fetch(s, light_entry(s, uSel));
+#if WF_EARLY >= 2
+    Taps4 envTaps;
+    if (s.has_hdr) envTaps = taps_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
+#endif
+#endif
     Material m = get_material(s, hmat);
+#if WF_EARLY >= 1
+    asm volatile("" ::: "memory");
+#endif
     if (htex != -1) {
         if (texture_bound(s, htex)) m.baseColor = albedo_resolve(albedo_fetch(s, htex, q.u, q.v));
         else m.baseColor = mk3(0.f, 0.f, 0.f);                                        // unbound unit -> 0
@@ -182,10 +194,10 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     // direct light (:878-909): candidate values, used if the shadow ray is unoccluded
     f3 LD = mk3(0.f, 0.f, 0.f);
     float pl = 0.f;
-    const float uSel = rand01(seed);
     if (s.n_lights > 0) {                            // light_index() == -1 iff no lights
+#if WF_EARLY < 1
         const LightFetch lf = light_fetch(s, light_entry(s, uSel));
-        float u0 = rand01(seed), u1 = rand01(seed);
+#endif
         float su0 = sqrtf(u0);
         float bx = 1.0f - su0, by = u1 * su0, bz = (1.0f - bx) - by;
         f3 p0 = mk3(lf.va0.x, lf.va0.y, lf.va0.z), p1 = mk3(lf.va1.x, lf.va1.y, lf.va1.z);
@@ -214,9 +226,12 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
     if (s.has_hdr) {
-        float r1 = rand01(seed), r2 = rand01(seed);
         f3 enL;
+#if WF_EARLY >= 2
+        f3 enLi = taps_resolve(env_dir(s, envTaps, enL, pe));
+#else
         f3 enLi = sample_env(s, r1, r2, enL, pe);
+#endif
         if (dot(enL, N) > 0) {
             f3 dB = disney(bc, enL);
             LE = divs(muls(mul(dB, enLi), dot(enL, N)), pe);
@@ -288,28 +303,39 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
 #ifndef WF_SORT_OCTANT
 #define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
 #endif
+#ifndef WF_SORT_SUB
+#define WF_SORT_SUB 1      // direction bins per octant (1, or 3: + the dominant axis)
+#endif
+#define WF_NBIN (8 * WF_SORT_SUB)
+PN_DEV int wf_dir_bin(const f3 d) {
+    const int oct = WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
+    if (WF_SORT_SUB == 1) return oct;
+    const float ax = pnm_fabs(d.x), ay = pnm_fabs(d.y), az = pnm_fabs(d.z);
+    const int dom = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
+    return oct * WF_SORT_SUB + dom;
+}
 PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays) {
-    // Inside a segment the rays are grouped by direction octant: rays with the
-    // same signs take the same near/far choice at every node (:448), so a wave
-    // walks the tree more coherently.  Slots within an octant come from LDS
-    // atomics (order not deterministic, which no result depends on).
-    __shared__ unsigned int bin[3][9];
+    // Inside a segment the rays are grouped by direction bin: rays with the same
+    // signs take the same near/far choice at every node (:448), so a wave walks
+    // the tree more coherently.  Slots within a bin come from LDS atomics (order
+    // not deterministic, which no result depends on).
+    __shared__ unsigned int bin[3][WF_NBIN + 1];
     const uint32_t need[3] = {WF_RLIGHT, WF_RENV, WF_RCONT};
-    if (threadIdx.x < 27) (&bin[0][0])[threadIdx.x] = 0;
+    for (int k = threadIdx.x; k < 3 * (WF_NBIN + 1); k += blockDim.x) (&bin[0][0])[k] = 0;
     __syncthreads();
     int oct[3];
     unsigned int rank[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
-        oct[k] = WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
+        oct[k] = wf_dir_bin(d);
         rank[k] = (nfl & need[k]) ? atomicAdd(&bin[k][oct[k]], 1u) : 0u;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {                    // exclusive prefix over the octants of a kind
+    if (threadIdx.x < 3) {                    // exclusive prefix over the bins of a kind
         unsigned int run = 0;
-        for (int o = 0; o < 8; ++o) { const unsigned int c = bin[threadIdx.x][o]; bin[threadIdx.x][o] = run; run += c; }
-        bin[threadIdx.x][8] = run;
+        for (int o = 0; o < WF_NBIN; ++o) { const unsigned int c = bin[threadIdx.x][o]; bin[threadIdx.x][o] = run; run += c; }
+        bin[threadIdx.x][WF_NBIN] = run;
         b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] = run;
     }
     __syncthreads();
@@ -437,14 +463,20 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_DIAG_NOSTORE
 #define WF_DIAG_NOSTORE 0   // timing experiment: drop the trace results (wrong images)
 #endif
+#ifndef WF_DIAG_VALU
+#define WF_DIAG_VALU 0      // timing diagnostic: extra VALU instructions per traversal step
+#endif
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
 #ifndef WF_QSHARDS
 #define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
 #endif
-#ifndef WF_QBAND
-#define WF_QBAND 0          // experiment: shard = image band instead of interleaved items
+#ifndef WF_TREELET
+#define WF_TREELET 0        // top nodes kept in LDS (0 = off; <= 160 at 6 waves/SIMD)
+#endif
+#ifndef WF_PF
+#define WF_PF 0             // request the next dequeue ticket one segment ahead
 #endif
 #ifndef WF_QSTRIDE
 #define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
@@ -493,6 +525,16 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
+#if WF_TREELET
+    // the top WF_TREELET nodes (breadth-first numbering: the first indices) in LDS:
+    // node fetches there bypass the vector L1 / texture-address path
+    __shared__ float4 tnodes[WF_TREELET * 4];
+    {
+        const int nt4 = 4 * (s.n_nodes < WF_TREELET ? s.n_nodes : WF_TREELET);
+        for (int k = threadIdx.x; k < nt4; k += WF_TRACE_BLOCK) tnodes[k] = s.nodes[k];
+        __syncthreads();
+    }
+#endif
     const int tl = threadIdx.x, lane = tl & 63;
     // rays are dequeued one queue segment at a time (<= 256 rays of one kind from
     // 256 neighbouring paths, kind-major); one atomic per segment
@@ -501,6 +543,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     uint32_t n_rays = 0;
     uint32_t next = 0, end = 0, ckind = 0, qpart = 0;
     bool exhausted = false;
+    uint32_t pf_t = 0;          // WF_PF: dequeue ticket in flight (lane 0's value)
+    bool pf_valid = false;
 
     RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
     float tMax = 0.f;
@@ -525,21 +569,24 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 for (;;) {
                     const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
                     uint32_t t = 0;
-                    if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
-                    t = __builtin_amdgcn_readfirstlane(t);
-#if WF_QBAND
-                    // shard p = image band p (setup blocks [p n/S, (p+1) n/S)), kind-major
-                    const uint32_t lo = p * b.nseg_k / WF_QSHARDS, w = (p + 1) * b.nseg_k / WF_QSHARDS - lo;
-                    if (t < 3u * w * WF_NSUB) {
-                        const uint32_t kq = t / (w * WF_NSUB), r = t - kq * w * WF_NSUB;
-                        seg = (kq * b.nseg_k + lo + r / WF_NSUB) * WF_NSUB + r % WF_NSUB;
-                        break;
+                    if (WF_PF && pf_valid) {             // the ticket requested at the previous dequeue
+                        t = __builtin_amdgcn_readfirstlane(pf_t);
+                        pf_valid = false;
+                    } else {
+                        if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
+                        t = __builtin_amdgcn_readfirstlane(t);
                     }
-#else
                     const uint32_t item = t * WF_QSHARDS + p;
                     if (item < nseg) { seg = item; break; }
-#endif
                     if (++qpart == WF_QSHARDS) break;
+                }
+                if (WF_PF && seg < nseg) {
+                    // request the next ticket now: the atomic's latency passes while this
+                    // segment's rays are traced (its value is read at the next dequeue)
+                    const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
+                    pf_t = 0;
+                    if (lane == 0) pf_t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
+                    pf_valid = true;
                 }
                 if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
                 else {
@@ -611,8 +658,19 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     const bool isNode = !isTri & (cur != REF_NONE);
                     // ---- the step's single fetch: a triangle record or a node (lanes
                     // with neither re-read node 0, which stays in L1)
+#if WF_TREELET
+                    float4 q0, q1, q2, q3;
+                    if (!isTri & (!isNode | (cur < (uint32_t)WF_TREELET))) {     // treelet node (or node 0)
+                        const float4* ln = tnodes + 4 * (isNode ? cur : 0u);
+                        q0 = ln[0]; q1 = ln[1]; q2 = ln[2]; q3 = ln[3];
+                    } else {
+                        const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)cur;
+                        q0 = base[0]; q1 = base[1]; q2 = base[2]; q3 = base[3];
+                    }
+#else
                     const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)(isNode ? cur : 0u);
                     const float4 q0 = base[0], q1 = base[1], q2 = base[2], q3 = base[3];
+#endif
                     // triangle test (:254-357 / :360-424)
                     float e0, e1, e2, det, ts;
                     const bool acc = tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts) & isTri;
@@ -666,6 +724,14 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         busy = 0;
                     }
                 }
+#if WF_DIAG_VALU
+                {   // timing diagnostic: extra VALU per iteration (is the loop issue-bound?)
+                    float d = __int_as_float(lt);
+#pragma unroll
+                    for (int q = 0; q < WF_DIAG_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
+                    lt = __float_as_int(d) == 0x7fffffff ? 0 : lt;
+                }
+#endif
                 if (__popcll(__ballot(busy != 0)) <= thr) break;
             }
         };
