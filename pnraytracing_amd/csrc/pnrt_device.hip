@@ -335,7 +335,9 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     {
         ProfScope ps(c, PNRT_K_PRIMARY, w0);
-        hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
+        const unsigned ptiles = PT_PRIM_TILE ? (unsigned)(((c->width + 15) / 16) * ((fp.rows + 15) / 16))
+                                             : (unsigned)((pix + 255) / 256);
+        hipLaunchKernelGGL(pt_primary_kernel, dim3(ptiles), dim3(256), 0, w0, s, fp, P.primary);
     }
     HIPCHK(c, hipGetLastError());
     if (w1 != w0) {

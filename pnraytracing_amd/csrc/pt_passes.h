@@ -15,12 +15,90 @@ PN_DEV f3 camera_dir(const FrameParams& fp, int px, int py) {
 }
 
 // ---- primary hits (once per call) ------------------------------------------------------------
+#ifndef PT_PRIM_TILE
+#define PT_PRIM_TILE 0       // primary pass: one workgroup per 16x16-pixel tile (measured slower) or 256 pixels of a row
+#endif
+#ifndef PT_PRIM_STK
+#define PT_PRIM_STK 8        // primary pass: stack entries per lane in LDS (deeper ones in private memory)
+#endif
+// BVHIntersect (:429-461) for the primary pass: traverse<false>'s visit order and
+// culling, its far-child stack in LDS (entry k of lane tl at lds[k * 256 + tl]).
+PN_DEV bool traverse_closest_lds(const DevScene& s, const RayP& r, float& tMax, int& hitTri, uint2* lds, int tl) {
+    float zlo, zhi;
+    if (!box_test(r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                  s.root_max[2], zlo, zhi))
+        return false;
+    uint2 spill[PT_STACK];
+    int sp = 0;
+    uint32_t cur = s.root_ref;
+    bool hit = false;
+    const float cullScale = 1.000001f;
+    for (;;) {
+        if (!(cur & REF_LEAF)) {
+            const float4* n = s.nodes + 4 * (size_t)cur;
+            float4 a = n[0], b = n[1], c = n[2];
+            uint4 m = *reinterpret_cast<const uint4*>(n + 3);
+            float tmc = tMax * cullScale;
+            float zloL, zhiL, zloR, zhiR;
+            bool hL = box_test(r, a.x, a.y, a.z, a.w, b.x, b.y, zloL, zhiL);
+            bool hR = box_test(r, b.z, b.w, c.x, c.y, c.z, c.w, zloR, zhiR);
+            if (hL && zcull(r, zloL, zhiL, tmc)) hL = false;
+            if (hR && zcull(r, zloR, zhiR, tmc)) hR = false;
+            bool rightFirst = comp(r.d, (int)m.z) < 0;       // :448
+            uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+            bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+            float zFar = rightFirst ? zloL : zloR;
+            if (hNear) {
+                if (hFar) {
+                    const uint2 e = make_uint2(farRef, __float_as_uint(zFar));
+                    if (sp < PT_PRIM_STK) lds[sp * 256 + tl] = e; else spill[sp - PT_PRIM_STK] = e;
+                    ++sp;
+                }
+                cur = nearRef;
+                continue;
+            }
+            if (hFar) { cur = farRef; continue; }
+        } else {
+            int start, cnt;
+            decode_leaf(s, cur, start, cnt);
+            for (int i = start; i < start + cnt; ++i) {
+                const float4* t = s.tris + 3 * (size_t)i;
+                float e0, e1, e2, det, ts;
+                if (tri_test(r, t[0], t[1], t[2], tMax, e0, e1, e2, det, ts)) {
+                    tMax = ts * (1.0f / det);
+                    hitTri = i;
+                    hit = true;
+                }
+            }
+        }
+        // pop (far children re-checked against the tMax found meanwhile)
+        for (;;) {
+            if (sp == 0) return hit;
+            --sp;
+            const uint2 e = sp < PT_PRIM_STK ? lds[sp * 256 + tl] : spill[sp - PT_PRIM_STK];
+            cur = e.x;
+            const float z = __uint_as_float(e.y);
+            if (!(r.cull_ok() && z > tMax * cullScale && z > 1e-20f)) break;
+        }
+    }
+}
+
 // record: q0 = (P.xyz, bits(mat)), q1 = (N.xyz, u), q2 = (v, base.xyz); mat = -1 on a miss
-// (base = emissive of the hit material, or the env colour of the primary direction)
+// (base = emissive of the hit material, or the env colour of the primary direction).
+// One workgroup per 16x16-pixel tile (coherent camera rays).
 __global__ void __launch_bounds__(256) pt_primary_kernel(DevScene s, FrameParams fp, float4* rec) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= fp.rows * fp.width) return;
-    int lr = i / fp.width, px = i - lr * fp.width;
+    __shared__ uint2 lds[(PT_PRIM_STK > 0 ? PT_PRIM_STK : 1) * 256];
+#if PT_PRIM_TILE
+    const int tiles_x = (fp.width + 15) / 16;
+    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+    const int px = tx * 16 + (threadIdx.x & 15), lr = ty * 16 + (threadIdx.x >> 4);
+    if (px >= fp.width || lr >= fp.rows) return;
+    const size_t i = (size_t)lr * fp.width + px;
+#else
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (size_t)fp.rows * fp.width) return;
+    const int lr = (int)(i / fp.width), px = (int)(i - (size_t)lr * fp.width);
+#endif
     int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
     f3 eye = mk3(fp.eye[0], fp.eye[1], fp.eye[2]);
     f3 dir = camera_dir(fp, px, py);
@@ -28,7 +106,7 @@ __global__ void __launch_bounds__(256) pt_primary_kernel(DevScene s, FrameParams
     float tmax = PT_FLOAT_MAX;
     int hitTri = -1;
     float4 q0, q1, q2;
-    if (traverse<false>(s, r, tmax, hitTri)) {
+    if (PT_PRIM_STK > 0 ? traverse_closest_lds(s, r, tmax, hitTri, lds, threadIdx.x) : traverse<false>(s, r, tmax, hitTri)) {
         Hit h = make_hit(s, r, hitTri);
         f3 em = get_emissive(s, h.mat);
         q0 = make_float4(h.P.x, h.P.y, h.P.z, __int_as_float(h.mat));
@@ -41,9 +119,9 @@ __global__ void __launch_bounds__(256) pt_primary_kernel(DevScene s, FrameParams
         q1 = make_float4(0.f, 0.f, 0.f, 0.f);
         q2 = make_float4(0.f, c.x, c.y, c.z);
     }
-    rec[3 * (size_t)i] = q0;
-    rec[3 * (size_t)i + 1] = q1;
-    rec[3 * (size_t)i + 2] = q2;
+    rec[3 * i] = q0;
+    rec[3 * i + 1] = q1;
+    rec[3 * i + 2] = q2;
 }
 
 // Frame-ordered progressive mean (ray_tracing.comp:988-991) of one chunk.

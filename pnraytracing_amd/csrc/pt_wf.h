@@ -472,6 +472,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_QSHARDS
 #define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
 #endif
+#ifndef WF_Q3_SHARED
+#define WF_Q3_SHARED 1      // triangle lanes' unused fourth 16-B load goes to one shared address
+#endif
 #ifndef WF_TREELET
 #define WF_TREELET 0        // top nodes kept in LDS (0 = off; <= 160 at 6 waves/SIMD)
 #endif
@@ -669,7 +672,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     }
 #else
                     const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)(isNode ? cur : 0u);
-                    const float4 q0 = base[0], q1 = base[1], q2 = base[2], q3 = base[3];
+                    // WF_Q3_SHARED: triangle lanes read the fourth quarter from one shared
+                    // address (one cache access per wave instead of one per lane)
+                    const float4* b3 = (WF_Q3_SHARED && isTri) ? s.zero4 : base + 3;
+                    const float4 q0 = base[0], q1 = base[1], q2 = base[2], q3 = *b3;
 #endif
                     // triangle test (:254-357 / :360-424)
                     float e0, e1, e2, det, ts;
