@@ -11,7 +11,7 @@ import numpy as np
 import pyoracle
 from pnraytracing_amd import scenes as S
 
-STEP = {"C2": 9, "C4": 9, "C5": 45}      # every k-th row (oracle cost bound)
+STEP = {"C2": 9, "C3": 9, "C4": 9, "C5": 45}      # every k-th row (oracle cost bound)
 out_path = os.path.join(REPO, "profiles", "algorithmic_bytes.json")
 res = json.load(open(out_path)) if os.path.exists(out_path) else {}
 for name in sys.argv[1:] or ["C2", "C4"]:

@@ -9,7 +9,7 @@ import collections, csv, glob, json, os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 cfg = sys.argv[1]
 rows = int(sys.argv[2]) if len(sys.argv) > 2 else 1080
-root = os.path.join(REPO, "gpurun_out", "pmc")
+root = os.environ.get("PMC_ROOT") or os.path.join(REPO, "gpurun_out", "pmc")
 SHORT = {"pt_wf_trace": "trace", "pt_wf_setup": "setup", "pt_wf_shade": "shade", "pt_wf_gen": "gen",
          "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
          "pt_primary_kernel": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
