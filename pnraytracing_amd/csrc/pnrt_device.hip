@@ -202,15 +202,28 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 // Wavefront buffers of one batch of n path slots, carved from `base`.
 static size_t wf_bytes(size_t n) {
     const size_t npad = (n + 255) / 256 * 256;
-    return n * (16 * 7 + 4 + 4 + 2) + 256 + npad * 96 + (npad / 256) * 12 + 256 + 2048 + 256 + 512 +
-           (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
+    return 2 * (npad * 16 * 7 + (npad / 256) * 4 + 256) + n * (4 + 2) + 256 + npad * 96 + (npad / 256) * 12 + 256 +
+           2048 + 256 + 512 + (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
 }
-static WfBufs wf_layout(char* base, size_t n) {
+// The two path-state sets of a batch (entries are indexed up to npad: a block's
+// live paths are compacted to the front of its 256 entries).
+struct WfLayout {
     WfBufs b;
-    float4** f4[] = {&b.P0, &b.P1, &b.P2, &b.P3, &b.P4, &b.P5, &b.P6};
+    PathSet set[2];
+};
+static WfLayout wf_layout(char* base, size_t n) {
+    WfLayout L;
+    WfBufs& b = L.b;
+    const size_t npad = (n + 255) / 256 * 256;
     size_t off = 0;
-    for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += n * 16; }
-    b.flags = reinterpret_cast<uint32_t*>(base + off); off += n * 4;
+    for (PathSet& ps : L.set) {
+        float4** f4[] = {&ps.P0, &ps.P1, &ps.P2, &ps.P3, &ps.P4, &ps.P5, &ps.P6};
+        for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += npad * 16; }
+        ps.bcount = reinterpret_cast<uint32_t*>(base + off); off += (npad / 256) * 4;
+        off = (off + 255) & ~(size_t)255;
+    }
+    b.rd = L.set[1];
+    b.wr = L.set[0];
     b.hit = reinterpret_cast<int*>(base + off); off += n * 4;
     b.occ = reinterpret_cast<uint8_t*>(base + off); off += n * 2;
     off = (off + 255) & ~(size_t)255;
@@ -223,14 +236,17 @@ static WfBufs wf_layout(char* base, size_t n) {
     b.counter = reinterpret_cast<unsigned int*>(base + off);               // 8 counters, 256 B apart
     b.stats = reinterpret_cast<unsigned long long*>(base + off + 2048);
     b.n = (uint32_t)n;
-    return b;
+    return L;
 }
 
 // One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
 // its colours land in frame slots [0, cf) of `colors`.
-static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, WfBufs b, hipStream_t st,
+static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, const WfLayout& L, hipStream_t st,
                         const float4* primary, float4* colors) {
+    WfBufs b = L.b;
+    if (b.n > WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: too many paths per batch");
     const dim3 g((unsigned)((b.n + 255) / 256));
+    b.wr = L.set[0];
     {   // path state + bounce-0 sampling
         ProfScope ps(c, PNRT_K_GEN, st);
         hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
@@ -275,7 +291,9 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, W
         }
         {
             ProfScope ps(c, PNRT_K_SHADE, st);
-            // MIS + continuation, then the next bounce's sampling
+            // MIS + continuation, then the next bounce's sampling (sets alternate)
+            b.rd = L.set[bounce & 1];
+            b.wr = L.set[(bounce + 1) & 1];
             hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
         }
         HIPCHK(c, hipGetLastError());
@@ -348,23 +366,23 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         const uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
         const uint32_t cfA = split && cf >= 2 ? (cf + 1) / 2 : cf, cfB = cf - cfA;
         char* base = static_cast<char*>(P.wf);
-        WfBufs a = wf_layout(base, per_frame * cfA);
-        a.ovf = P.ovf[0];
-        a.ovf_stride = (uint32_t)ovf_stride;
-        a.chunk_frames = (int)cfA;
-        a.tiles_x = tiles_x;
-        a.first_frame = first + f0;
+        WfLayout a = wf_layout(base, per_frame * cfA);
+        a.b.ovf = P.ovf[0];
+        a.b.ovf_stride = (uint32_t)ovf_stride;
+        a.b.chunk_frames = (int)cfA;
+        a.b.tiles_x = tiles_x;
+        a.b.first_frame = first + f0;
         if (f0) {                        // the previous group's blend has read the colours
             HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
             if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));
         }
         if (cfB) {
-            WfBufs bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
-            bb.ovf = P.ovf[1];
-            bb.ovf_stride = (uint32_t)ovf_stride;
-            bb.chunk_frames = (int)cfB;
-            bb.tiles_x = tiles_x;
-            bb.first_frame = first + f0 + cfA;
+            WfLayout bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
+            bb.b.ovf = P.ovf[1];
+            bb.b.ovf_stride = (uint32_t)ovf_stride;
+            bb.b.chunk_frames = (int)cfB;
+            bb.b.tiles_x = tiles_x;
+            bb.b.first_frame = first + f0 + cfA;
             if ((rc = render_batch(c, s, fp, bb, w1, P.primary, P.colors + (size_t)cfA * pix))) return rc;
             HIPCHK(c, hipEventRecord(P.ev_join[1], w1));
             HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[1], 0));

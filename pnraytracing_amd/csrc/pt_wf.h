@@ -35,25 +35,36 @@
 #define WF_TRACE_BLOCK 256
 #define WF_CHUNK 256u        // rays per dequeue
 
-// flags[path]: bit0 alive, bit1 light ray, bit2 env ray, bit3 continuation ray,
-// bits 8..10 bounce
-#define WF_ALIVE 1u
+// ray kinds a setup emitted (enqueue) ...
 #define WF_RLIGHT 2u
 #define WF_RENV 4u
 #define WF_RCONT 8u
+// ... and the path's meta word, P6.w: slot (pixel, frame) | light ray | env ray | bounce
+#define WF_META_SLOT 0x03ffffffu
+#define WF_META_RL (1u << 26)
+#define WF_META_RE (1u << 27)
+#define WF_META_BSHIFT 28
 
-struct WfBufs {
-    // path state between setup and shade: exactly what shade reads, 112 B per
-    // path (the primary hit's base colour is re-read from the primary record)
+// Path state between a setup and the next shade: exactly what shade reads,
+// 112 B per live path (the primary hit's base colour is re-read from the
+// primary record).  A setup block writes its live paths compacted to the front
+// of its 256-entry range (entry j = 256 * block + rank), so the next shade's
+// lanes are all live paths and its empty waves exit at once; two sets
+// alternate by bounce (a shade reads one and its setup writes the other).
+struct PathSet {
     float4* P0;   // continuation origin (P + N*1e-4).xyz, dPDF
     float4* P1;   // L.xyz, |N.L|
     float4* P2;   // dBRDF.xyz, enPDF
     float4* P3;   // LDirect.xyz, lightPDF  written iff the path has a light ray, read iff it is unoccluded
     float4* P4;   // LEnvironment.xyz, -    written iff the path has an env ray, read iff it is unoccluded
     float4* P5;   // Lo.xyz, bits(seed)
-    float4* P6;   // throughput.xyz, -      written from bounce 1 on (bounce 0: (1, 1, 1))
-    uint32_t* flags;   // dense: paths that end are cleared with coalesced 4-B stores
-    // trace results
+    float4* P6;   // throughput.xyz, bits(meta)
+    uint32_t* bcount;   // live paths of each setup block
+};
+
+struct WfBufs {
+    PathSet rd, wr;    // shade reads rd; its setup (and gen) writes wr
+    // trace results, by path entry j
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
     uint2* ovf;        // traversal stack spill, ovf_stride entries per trace lane
@@ -63,7 +74,7 @@ struct WfBufs {
     // paths' rays of kind k (light | env | continuation) into segment (k, j) =
     // slots [k * npad + 256 j, +segcount[k * nseg_k + j]) as ready-to-trace
     // records: rayO = (origin, bits(path slot)), rayD = (direction, -)
-    float4* rayO;            // [3 * npad]
+    float4* rayO;            // [3 * npad]  (.w = path entry j)
     float4* rayD;            // [3 * npad]
     unsigned int* segcount;  // [3 * nseg_k]
     uint32_t npad;           // n rounded up to 256
@@ -87,8 +98,28 @@ PN_DEV void wf_coords(const WfBufs& b, uint32_t s, int& x, int& lr, int& k) {
     lr = ty * 8 + (p >> 3);
 }
 
-// a path slot that ends (or never starts) is marked dead
-PN_DEV void wf_kill(const WfBufs& b, uint32_t i) { b.flags[i] = 0u; }
+// Number of set bits of m below this lane (v_mbcnt).
+PN_DEV uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// Rank of this lane among the lanes of its 256-thread block with `live` set
+// (wave ballots + LDS), and the block's total; every thread must call it.
+PN_DEV uint32_t wf_block_rank(bool live, uint32_t& total) {
+    __shared__ uint32_t wc[4];
+    const uint64_t m = __ballot(live);
+    const int w = (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t c = wc[k];
+        base += k < w ? c : 0u;
+        tot += c;
+    }
+    total = tot;
+    return base + lanes_below(m);
+}
 
 PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
     color = mk3(clampf(color.x, 0.f, 1.f), clampf(color.y, 0.f, 1.f), clampf(color.z, 0.f, 1.f));
@@ -155,10 +186,11 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
 #ifndef WF_EARLY
 #define WF_EARLY 1          // 1: light record fetched with the material, 2: + the env table taps
 #endif
-// Returns the path's flags for the bounce (alive, bounce, which rays exist);
-// writes the path state P0-P6; the rays go to `rays`.
-PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, int bounce,
-                              int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
+// Returns the ray kinds the bounce emits; writes the path state P0-P6 of entry
+// i of the write set (slot = the path's (pixel, frame) slot); the rays go to `rays`.
+PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t slot,
+                              int bounce, int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
+    const PathSet& w = b.wr;
     const f3 P = q.P, N = q.N, V = q.V;
     const int hmat = q.mt & 0x00ffffff, htex = (int)((uint32_t)q.mt >> 24) - 1;
     uint32_t seed = q.seed;
@@ -189,7 +221,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     else T = normalize(cross(N, mk3(0.f, 0.f, 1.f)));
     B = cross(N, T);
     BrdfCtx bc = brdf_prepare(V, N, T, B, m);
-    uint32_t nfl = WF_ALIVE | ((uint32_t)bounce << 8);
+    uint32_t nfl = 0;
 
     // direct light (:878-909): candidate values, used if the shadow ray is unoccluded
     f3 LD = mk3(0.f, 0.f, 0.f);
@@ -221,7 +253,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     // stored as soon as final (shorter live ranges), and only when shade can use it:
     // shade takes (0, 0) for a path without a light ray, as the reference's
     // initial LDirect / lightPDF (:878-879)
-    if (!WF_KO_P34 && (nfl & WF_RLIGHT)) b.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);
+    if (!WF_KO_P34 && (nfl & WF_RLIGHT)) w.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -239,7 +271,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
-    if (!WF_KO_P34 && (nfl & WF_RENV)) b.P4[i] = make_float4(LE.x, LE.y, LE.z, 0.f);
+    if (!WF_KO_P34 && (nfl & WF_RENV)) w.P4[i] = make_float4(LE.x, LE.y, LE.z, 0.f);
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -288,12 +320,13 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     rays.dC = L;
     rays.oP = P;
     rays.oOff = add(P, muls(N, 0.0001f));
-    b.P0[i] = make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF);
-    b.P1[i] = make_float4(L.x, L.y, L.z, NdotL);
-    b.P2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe);
-    b.flags[i] = nfl | WF_RCONT;
-    b.P5[i] = make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed));
-    if (bounce > 0) b.P6[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, 0.f);
+    const uint32_t meta = slot | ((nfl & WF_RLIGHT) ? WF_META_RL : 0u) | ((nfl & WF_RENV) ? WF_META_RE : 0u) |
+                          ((uint32_t)bounce << WF_META_BSHIFT);
+    w.P0[i] = make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF);
+    w.P1[i] = make_float4(L.x, L.y, L.z, NdotL);
+    w.P2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe);
+    w.P5[i] = make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed));
+    w.P6[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(meta));
     return nfl | WF_RCONT;
 }
 
@@ -358,13 +391,14 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
 // ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
 __global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
                                                        float4* colors) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t nfl = 0;
-    BounceRays rays;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     // path slot
+    bool cont = false;
+    PathIn q;
+    int x = 0, py = 0;
+    uint32_t frame = 0;
     if (i < b.n) {
-        int x, lr, k;
+        int lr, k;
         wf_coords(b, i, x, lr, k);
-        wf_kill(b, i);
         if (x < fp.width && lr < fp.rows) {
             const float4* rec = primary + 3 * ((size_t)lr * fp.width + x);
             const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
@@ -375,20 +409,25 @@ __global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_gen_setup(DevScene 
             } else if (fp.max_depth == 0) {
                 wf_write_color(fp, colors, k, lr, x, add(base, mk3(0.f, 0.f, 0.f)));
             } else {
-                const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
-                const uint32_t frame = b.first_frame + (uint32_t)k;
-                PathIn q;
+                py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+                frame = b.first_frame + (uint32_t)k;
                 q.P = mk3(q0.x, q0.y, q0.z); q.N = mk3(q1.x, q1.y, q1.z);
                 q.u = q1.w; q.v = q2.x; q.mt = mt;
                 q.V = neg(camera_dir(fp, x, py));
                 q.cw = mk3(1.f, 1.f, 1.f);
                 q.Lo = mk3(0.f, 0.f, 0.f);
                 q.seed = ((uint32_t)x * 1973u + (uint32_t)py * 9277u + frame * 26699u) | 1u;
-                nfl = wf_setup_core(s, fp, b, i, 0, x, py, frame, q, rays);
+                cont = true;
             }
         }
     }
-    wf_enqueue(b, i, nfl, rays);     // every lane of the wave reaches this point
+    uint32_t total;
+    const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);    // compacted path entry
+    uint32_t nfl = 0;
+    BounceRays rays;
+    if (cont) nfl = wf_setup_core(s, fp, b, j, i, 0, x, py, frame, q, rays);
+    if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
+    wf_enqueue(b, j, nfl, rays);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
@@ -396,11 +435,6 @@ __global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_gen_setup(DevScene 
 PN_DEV uint2* wf_ovf(const WfBufs& b, int tl) {
     return b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride;
 }
-// Number of set bits of m below this lane (v_mbcnt).
-PN_DEV uint32_t lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 // Leaf ref -> triangle range; the leaf-table lookup is behind a scene-uniform
 // (scalar) branch, so scenes without table leaves pay no divergent branch.
 PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& cnt) {
@@ -753,13 +787,13 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 }
 
 // ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
-PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, const float4* primary,
-                              float4* colors, uint32_t i, BounceRays& rays) {
-    const uint32_t fl = b.flags[i];
-    if (!(fl & WF_ALIVE)) return 0;
-    int bounce = (int)((fl >> 8) & 7u);
-    const float4 p0 = b.P0[i], p1 = b.P1[i], p2 = b.P2[i], p5 = b.P5[i];
-    const float4 p6 = bounce > 0 ? b.P6[i] : make_float4(1.f, 1.f, 1.f, 0.f);   // bounce 0: throughput (1, 1, 1)
+// Path entry i of the read set.  Returns whether the path continues; then q,
+// bounce, slot and the pixel / frame carry its next bounce to the setup.
+PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs& b, const float4* primary,
+                          float4* colors, uint32_t i, PathIn& q, int& bounce, uint32_t& slot, int& x, int& py,
+                          uint32_t& frame) {
+    const PathSet& rd = b.rd;
+    const float4 p0 = rd.P0[i], p1 = rd.P1[i], p2 = rd.P2[i], p5 = rd.P5[i], p6 = rd.P6[i];
     const int ht = b.hit[i];
     // the light / env candidates are read only where they count: an occluded
     // light ray zeroes LDirect and lightPDF (:890), an occluded or absent env ray
@@ -767,13 +801,16 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
     // read the scene's zero float4 instead (no branch: both loads issue together).
     const uint32_t oc = reinterpret_cast<const uint16_t*>(b.occ)[i];      // both bytes in one load
     asm volatile("" ::: "memory");     // keep the hit load in this first batch (the scheduler sinks it)
-    const bool useL = (fl & WF_RLIGHT) && !(oc & 0xffu);
-    const bool useE = (fl & WF_RENV) && !(oc >> 8);
+    const uint32_t meta = __float_as_uint(p6.w);
+    bounce = (int)(meta >> WF_META_BSHIFT);
+    slot = meta & WF_META_SLOT;
+    const bool useL = (meta & WF_META_RL) && !(oc & 0xffu);
+    const bool useE = (meta & WF_META_RE) && !(oc >> 8);
     float4 p3, p4;
     if (WF_KO_P34) { p3 = make_float4(p2.x, 0.f, 0.f, 1.f); p4 = make_float4(p2.y, 0.f, 0.f, 1.f); }
     else {
-        p3 = *(useL ? b.P3 + i : s.zero4);
-        p4 = *(useE ? b.P4 + i : s.zero4);
+        p3 = *(useL ? rd.P3 + i : s.zero4);
+        p4 = *(useE ? rd.P4 + i : s.zero4);
     }
     // the continuation hit's records, in flight while the MIS sum waits for P3/P4
     // (a miss reads triangle 0's, unused)
@@ -787,8 +824,8 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
     float invPDFSum = 1.0f / ((pe + pl) + dPDF);
     f3 mis = add(muls(LE, pe), muls(LD, pl));
     Lo = add(Lo, muls(mul(cw, mis), invPDFSum));
-    int x, lr, k;
-    wf_coords(b, i, x, lr, k);
+    int lr, k;
+    wf_coords(b, slot, x, lr, k);
     if (ht < 0) {
         if (s.has_hdr) {
             f3 enLi = env_color(s, normalize(L));
@@ -796,8 +833,7 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
         }
         const float4 q2 = primary[3 * ((size_t)lr * fp.width + x) + 2];     // the primary hit's base colour
         wf_write_color(fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
-        wf_kill(b, i);
-        return 0;
+        return false;
     }
     RayP r = make_ray(mk3(p0.x, p0.y, p0.z), L, 0);        // the continuation ray as traced
     Hit h = hit_resolve(r, hf);
@@ -808,24 +844,39 @@ PN_DEV uint32_t wf_shade_path(const DevScene& s, const FrameParams& fp, const Wf
     if (bounce >= fp.max_depth) {
         const float4 q2 = primary[3 * ((size_t)lr * fp.width + x) + 2];
         wf_write_color(fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
-        wf_kill(b, i);
-        return 0;
+        return false;
     }
     // the next bounce starts here: its setup runs on the state in registers
-    PathIn q;
     q.P = h.P; q.N = h.N; q.u = h.u; q.v = h.v;
     q.mt = (h.mat & 0x00ffffff) | ((h.tex + 1) << 24);
     q.V = neg(L); q.cw = cw; q.Lo = Lo; q.seed = __float_as_uint(p5.w);
-    const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
-    return wf_setup_core(s, fp, b, i, bounce, x, py, b.first_frame + (uint32_t)k, q, rays);
+    py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+    frame = b.first_frame + (uint32_t)k;
+    return true;
 }
 
 // ---- shade + next-bounce setup: MIS, continuation hit (:936-972), then the next
 // bounce's sampling for the paths that continue ----------------------------------------------
 __global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
                                                          float4* colors) {
+    // the block's live paths are its first b.rd.bcount[block] entries
+    const uint32_t live = b.rd.bcount[blockIdx.x];
+    if (live == 0) {                          // no path: nothing to shade, no rays, empty next block
+        if (threadIdx.x < 3) b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] = 0u;
+        if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = 0u;
+        return;
+    }
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool cont = false;
+    PathIn q;
+    int bounce = 0, x = 0, py = 0;
+    uint32_t slot = 0, frame = 0;
+    if (threadIdx.x < live) cont = wf_shade_path(s, fp, b, primary, colors, i, q, bounce, slot, x, py, frame);
+    uint32_t total;
+    const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);
+    uint32_t nfl = 0;
     BounceRays rays;
-    const uint32_t nfl = i < b.n ? wf_shade_path(s, fp, b, primary, colors, i, rays) : 0u;
-    wf_enqueue(b, i, nfl, rays);     // every lane of the wave reaches this point
+    if (cont) nfl = wf_setup_core(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
+    if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
+    wf_enqueue(b, j, nfl, rays);     // every lane of the wave reaches this point
 }
