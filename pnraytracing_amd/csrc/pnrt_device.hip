@@ -294,7 +294,10 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             // MIS + continuation, then the next bounce's sampling (sets alternate)
             b.rd = L.set[bounce & 1];
             b.wr = L.set[(bounce + 1) & 1];
-            hipLaunchKernelGGL(pt_wf_shade_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
+            if (bounce + 1 == fp.max_depth)   // every path ends: no setup half, no rays
+                hipLaunchKernelGGL(pt_wf_shade_setup<true>, g, dim3(256), 0, st, s, fp, b, primary, colors);
+            else
+                hipLaunchKernelGGL(pt_wf_shade_setup<false>, g, dim3(256), 0, st, s, fp, b, primary, colors);
         }
         HIPCHK(c, hipGetLastError());
     }

@@ -856,9 +856,11 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
 }
 
 // ---- shade + next-bounce setup: MIS, continuation hit (:936-972), then the next
-// bounce's sampling for the paths that continue ----------------------------------------------
-__global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
-                                                         float4* colors) {
+// bounce's sampling for the paths that continue.  FINAL: the last bounce (every
+// path ends here), compiled without the setup half -> fewer registers, more waves.
+template <bool FINAL>
+__global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b,
+                                                                     const float4* primary, float4* colors) {
     // the block's live paths are its first b.rd.bcount[block] entries
     const uint32_t live = b.rd.bcount[blockIdx.x];
     if (live == 0) {                          // no path: nothing to shade, no rays, empty next block
@@ -872,6 +874,7 @@ __global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_shade_setup(DevScen
     int bounce = 0, x = 0, py = 0;
     uint32_t slot = 0, frame = 0;
     if (threadIdx.x < live) cont = wf_shade_path(s, fp, b, primary, colors, i, q, bounce, slot, x, py, frame);
+    if (FINAL) return;                        // bounce + 1 == max_depth: cont is false for every path
     uint32_t total;
     const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);
     uint32_t nfl = 0;
