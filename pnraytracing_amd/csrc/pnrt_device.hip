@@ -254,7 +254,8 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
     HIPCHK(c, hipGetLastError());
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
         // segment dequeue counter (+ the WF_STATS census)
-        HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_STATS ? 2048 + 256 : 2048, st));
+        // (zeroed by the setup kernel that queued the rays; the census builds also memset)
+        if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 256, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, st, s, b,

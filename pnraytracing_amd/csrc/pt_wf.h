@@ -32,6 +32,12 @@
 #define WF_KO_P34 0         // timing diagnostic: light/env candidates not stored in the path state (wrong images)
 #endif
 #define WF_OVF 56
+#ifndef WF_QSHARDS
+#define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
+#endif
+#ifndef WF_QSTRIDE
+#define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
+#endif
 #define WF_TRACE_BLOCK 256
 #define WF_CHUNK 256u        // rays per dequeue
 
@@ -85,6 +91,12 @@ struct WfBufs {
     int tiles_x;
     uint32_t first_frame;
 };
+
+// A setup kernel's block 0 resets the dequeue counters of the trace launch that
+// follows it (the previous trace has completed: stream order).
+PN_DEV void wf_reset_counters(const WfBufs& b) {
+    if (blockIdx.x == 0 && threadIdx.x < WF_QSHARDS) b.counter[threadIdx.x * WF_QSTRIDE] = 0u;
+}
 
 // path slot -> (x, local row, frame slot): 8x8-pixel tiles, frame-major inside a
 // tile, so consecutive path slots (and the rays they spawn) are spatial neighbours
@@ -392,6 +404,7 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
 __global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
                                                        float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     // path slot
+    wf_reset_counters(b);
     bool cont = false;
     PathIn q;
     int x = 0, py = 0;
@@ -503,9 +516,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
-#ifndef WF_QSHARDS
-#define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
-#endif
 #ifndef WF_Q3_SHARED
 #define WF_Q3_SHARED 1      // triangle lanes' unused fourth 16-B load goes to one shared address
 #endif
@@ -514,9 +524,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #endif
 #ifndef WF_PF
 #define WF_PF 0             // request the next dequeue ticket one segment ahead
-#endif
-#ifndef WF_QSTRIDE
-#define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
 #endif
 #ifndef WF_SUB
 #define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
@@ -862,6 +869,7 @@ template <bool FINAL>
 __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b,
                                                                      const float4* primary, float4* colors) {
     // the block's live paths are its first b.rd.bcount[block] entries
+    if (!FINAL) wf_reset_counters(b);
     const uint32_t live = b.rd.bcount[blockIdx.x];
     if (live == 0) {                          // no path: nothing to shade, no rays, empty next block
         if (threadIdx.x < 3) b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] = 0u;
