@@ -55,7 +55,10 @@ def build_device(force=False, extra=()):
     deps = [os.path.join(CSRC, d) for d in DEVICE_DEPS] + [os.path.join(INC, "pnrt.h")]
     if force or extra or _stale(out, deps):
         cmd = [HIPCC, f"--offload-arch={ARCH}", os.environ.get("PNRT_OPT", "-O3"), "-std=c++17", "-fPIC", "-shared",
-               "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-rdc", "-I", INC,
+               "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-rdc",
+               # no SLP packing into v_pk_*_f32: the register pairs it needs cost the
+               # trace kernel a wave per SIMD and the setup kernels one
+               "-fno-slp-vectorize", "-I", INC,
                *extra, *[os.path.join(CSRC, s) for s in DEVICE_SRCS], "-o", out]
         _run(cmd)
     return out

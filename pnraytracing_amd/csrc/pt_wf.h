@@ -397,7 +397,7 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
 }
 
 #ifndef WF_SHADE_WAVES
-#define WF_SHADE_WAVES 4      // waves per SIMD for the gen/shade kernels (<= 128 VGPRs)
+#define WF_SHADE_WAVES 5      // waves per SIMD for the gen/shade kernels (<= 96 VGPRs without SLP packing)
 #endif
 
 // ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
@@ -564,7 +564,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 // wave-level decision (ballot) at a reconvergence point: the ray <-> lane
 // refill runs between traversal phases.
 #ifndef WF_TRACE_WAVES
-#define WF_TRACE_WAVES 6      // waves per SIMD (80 VGPRs; the few spills are the per-ray result addresses)
+#define WF_TRACE_WAVES 7      // waves per SIMD (72 VGPRs, built without SLP packing; 3 spilled values)
 #endif
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
