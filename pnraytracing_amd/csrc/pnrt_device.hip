@@ -286,9 +286,9 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             HIPCHK(c, hipStreamSynchronize(st));
             HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
             fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu pop-only=%llu "
-                    "refills=%llu rays=%llu  lane-steps/ray=%.1f\n", bounce, b.n, stt[0],
+                    "refills=%llu rays=%llu  lane-steps/ray=%.1f  continuation lane-steps=%.1f%%\n", bounce, b.n, stt[0],
                     stt[0] ? (double)stt[1] / stt[0] : 0.0, stt[2], stt[3], stt[4], stt[5], stt[6],
-                    stt[6] ? (double)stt[1] / stt[6] : 0.0);
+                    stt[6] ? (double)stt[1] / stt[6] : 0.0, stt[1] ? 100.0 * stt[7] / stt[1] : 0.0);
         }
         {
             ProfScope ps(c, PNRT_K_SHADE, st);
@@ -636,7 +636,24 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
 
     DevScene& s = c->scene;
     int rc;
-    if ((rc = upload(c, nodes, &s.nodes)) || (rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tris, &s.tris)) || (rc = upload(c, tidx, &s.tri_idx)) ||
+    {   // nodes and triangle records in one allocation: the trace kernel addresses both
+        // through one buffer resource with 32-bit offsets
+        const size_t nb = nodes.size() * 16, tb = tris.size() * 16;
+        if (nb + tb >= ((size_t)1 << 32) - 64)
+            return set_err(c, PNRT_E_SCENE, "scene too large: nodes + triangles must stay below 4 GiB");
+        void* g = nullptr;
+        HIPCHK(c, hipMalloc(&g, nb + tb));
+        c->scene_allocs.push_back(g);
+        if (nb) HIPCHK(c, hipMemcpy(g, nodes.data(), nb, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(static_cast<char*>(g) + nb, tris.data(), tb, hipMemcpyHostToDevice));
+        c->scene_bytes += (int64_t)(nb + tb);
+        s.nodes = static_cast<const float4*>(g);
+        s.tris = reinterpret_cast<const float4*>(static_cast<char*>(g) + nb);
+        s.geo_tri_off = (uint32_t)nb;
+        s.geo_zero_off = (uint32_t)(nb + (size_t)nt * 48);      // tris' zeroed tail record
+        s.geo_bytes = (uint32_t)(nb + tb);
+    }
+    if ((rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tidx, &s.tri_idx)) ||
         (rc = upload(c, verts, &s.verts)) || (rc = upload(c, mats, &s.materials)) || (rc = upload(c, lights, &s.lights)) ||
         (rc = upload(c, tattr, &s.tri_attr)) || (rc = upload(c, lrec, &s.light_rec)) ||
         (rc = upload(c, std::vector<float4>(1, make_float4(0.f, 0.f, 0.f, 0.f)), &s.zero4)))

@@ -516,6 +516,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
+#ifndef WF_BUFFER_FETCH
+#define WF_BUFFER_FETCH 1   // the step's fetch as buffer loads with 32-bit offsets (one resource for nodes + tris)
+#endif
 #ifndef WF_Q3_SHARED
 #define WF_Q3_SHARED 1      // triangle lanes' unused fourth 16-B load goes to one shared address
 #endif
@@ -566,9 +569,18 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 7      // waves per SIMD (72 VGPRs, built without SLP packing; 3 spilled values)
 #endif
+PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
+#if WF_BUFFER_FETCH
+    const __amdgpu_buffer_rsrc_t geo =
+        __builtin_amdgcn_make_buffer_rsrc((void*)s.nodes, (short)0, (int)s.geo_bytes, 0x00020000);
+#endif
 #if WF_TREELET
     // the top WF_TREELET nodes (breadth-first numbering: the first indices) in LDS:
     // node fetches there bypass the vector L1 / texture-address path
@@ -691,6 +703,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     st[2] += __popcll(__ballot(busy != 0 && lc > 0));
                     st[3] += __popcll(__ballot(busy != 0 && lc <= 0 && cur != REF_NONE));
                     st[4] += __popcll(__ballot(busy != 0 && lc <= 0 && cur == REF_NONE));
+                    st[7] += __popcll(__ballot(busy != 0 && (rid >> 30) == 2u));     // continuation-ray lane steps
                 }
                 if (busy) {
                     // One step, written branch-light: the triangle test and the node
@@ -712,11 +725,21 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         q0 = base[0]; q1 = base[1]; q2 = base[2]; q3 = base[3];
                     }
 #else
+#if WF_BUFFER_FETCH
+                    // nodes and triangle records through one buffer resource, 32-bit offsets
+                    const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)lt * 48u : (isNode ? cur : 0u) * 64u;
+                    // triangle lanes read the fourth quarter from one shared address (one
+                    // cache access per wave instead of one per lane)
+                    const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
+                    const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
+                                 q3 = geo_load(geo, off3);
+#else
                     const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)(isNode ? cur : 0u);
                     // WF_Q3_SHARED: triangle lanes read the fourth quarter from one shared
                     // address (one cache access per wave instead of one per lane)
                     const float4* b3 = (WF_Q3_SHARED && isTri) ? s.zero4 : base + 3;
                     const float4 q0 = base[0], q1 = base[1], q2 = base[2], q3 = *b3;
+#endif
 #endif
                     // triangle test (:254-357 / :360-424)
                     float e0, e1, e2, det, ts;
