@@ -397,11 +397,14 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
 }
 
 #ifndef WF_SHADE_WAVES
-#define WF_SHADE_WAVES 5      // waves per SIMD for the gen/shade kernels (<= 96 VGPRs without SLP packing)
+#define WF_SHADE_WAVES 5      // waves per SIMD for the shade/setup kernel (<= 96 VGPRs without SLP packing)
+#endif
+#ifndef WF_GEN_WAVES
+#define WF_GEN_WAVES WF_SHADE_WAVES   // waves per SIMD for the gen/setup kernel
 #endif
 
 // ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
-__global__ void __launch_bounds__(256, WF_SHADE_WAVES) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
+__global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
                                                        float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     // path slot
     wf_reset_counters(b);

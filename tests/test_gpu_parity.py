@@ -188,6 +188,21 @@ def test_progressive_split_calls(pt):
     assert_bitwise(b, a, "render(0,1)+render(1,3) vs render(0,4)")
 
 
+def test_many_frames_and_calls(pt):
+    """One call of 11 frames (two frame groups of <= 8 paths-per-pixel batches) and
+    six calls in a row (the pipelined buffer sets rotate twice) both equal the
+    oracle's 11 / 12-frame progressive means."""
+    c = cfg("C2", width=80, height=48, spp=4)
+    got = gpu_render(pt, c, 0, 11)
+    ref, _ = pyoracle.Oracle(c).render(0, 11)
+    assert_bitwise(got, ref, "render(0, 11)")
+    pt.reset_accum()
+    for k in range(6):
+        pt.render(2 * k, 2)
+    ref, _ = pyoracle.Oracle(c).render(0, 12)
+    assert_bitwise(pt.read_accum(), ref, "6 x render(2k, 2)")
+
+
 def test_shard_union_equals_full(pt):
     c = cfg("C2", width=200, height=100, spp=4)
     full = gpu_render(pt, c, 0, 2)
