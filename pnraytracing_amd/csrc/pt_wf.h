@@ -195,11 +195,16 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
     return f;
 }
 
-#ifndef WF_EARLY
-#define WF_EARLY 1          // 1: light record fetched with the material, 2: + the env table taps
+#ifndef WF_GEN_EARLY
+#define WF_GEN_EARLY 2      // gen: the env table taps fetched with the light record and the material
 #endif
+#ifndef WF_SHADE_EARLY
+#define WF_SHADE_EARLY 1    // shade: the light record with the material, the env taps later (registers)
+#endif
+// EARLY 1: the light record is fetched with the material; 2: the env table taps too.
 // Returns the ray kinds the bounce emits; writes the path state P0-P6 of entry
 // i of the write set (slot = the path's (pixel, frame) slot); the rays go to `rays`.
+template <int EARLY>
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t slot,
                               int bounce, int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const PathSet& w = b.wr;
@@ -212,18 +217,14 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     float u0 = 0.f, u1 = 0.f, r1 = 0.f, r2 = 0.f;
     if (s.n_lights > 0) { u0 = rand01(seed); u1 = rand01(seed); }
     if (s.has_hdr) { r1 = rand01(seed); r2 = rand01(seed); }
-#if WF_EARLY >= 1
     // light record (and env table taps) in flight with the material fetch
     const LightFetch lf = light_fetch(s, light_entry(s, uSel));
-#if WF_EARLY >= 2
     Taps4 envTaps;
-    if (s.has_hdr) envTaps = taps_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
-#endif
-#endif
+    if constexpr (EARLY >= 2) {
+        if (s.has_hdr) envTaps = taps_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
+    }
     Material m = get_material(s, hmat);
-#if WF_EARLY >= 1
     asm volatile("" ::: "memory");
-#endif
     if (htex != -1) {
         if (texture_bound(s, htex)) m.baseColor = albedo_resolve(albedo_fetch(s, htex, q.u, q.v));
         else m.baseColor = mk3(0.f, 0.f, 0.f);                                        // unbound unit -> 0
@@ -239,9 +240,6 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     f3 LD = mk3(0.f, 0.f, 0.f);
     float pl = 0.f;
     if (s.n_lights > 0) {                            // light_index() == -1 iff no lights
-#if WF_EARLY < 1
-        const LightFetch lf = light_fetch(s, light_entry(s, uSel));
-#endif
         float su0 = sqrtf(u0);
         float bx = 1.0f - su0, by = u1 * su0, bz = (1.0f - bx) - by;
         f3 p0 = mk3(lf.va0.x, lf.va0.y, lf.va0.z), p1 = mk3(lf.va1.x, lf.va1.y, lf.va1.z);
@@ -271,11 +269,9 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     float pe = 0.f;
     if (s.has_hdr) {
         f3 enL;
-#if WF_EARLY >= 2
-        f3 enLi = taps_resolve(env_dir(s, envTaps, enL, pe));
-#else
-        f3 enLi = sample_env(s, r1, r2, enL, pe);
-#endif
+        f3 enLi;
+        if constexpr (EARLY >= 2) enLi = taps_resolve(env_dir(s, envTaps, enL, pe));
+        else enLi = sample_env(s, r1, r2, enL, pe);
         if (dot(enL, N) > 0) {
             f3 dB = disney(bc, enL);
             LE = divs(muls(mul(dB, enLi), dot(enL, N)), pe);
@@ -441,7 +437,7 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
     const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);    // compacted path entry
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core(s, fp, b, j, i, 0, x, py, frame, q, rays);
+    if (cont) nfl = wf_setup_core<WF_GEN_EARLY>(s, fp, b, j, i, 0, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
     wf_enqueue(b, j, nfl, rays);     // every lane of the wave reaches this point
 }
@@ -913,7 +909,7 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
+    if (cont) nfl = wf_setup_core<WF_SHADE_EARLY>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
     wf_enqueue(b, j, nfl, rays);     // every lane of the wave reaches this point
 }
