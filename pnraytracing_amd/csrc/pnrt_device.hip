@@ -199,6 +199,13 @@ static int upload(pnrt_ctx* c, const std::vector<T>& v, const T** out) {
 
 static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 
+#ifndef WF_TRACE_GRID_PCT
+#define WF_TRACE_GRID_PCT 40         // cap of the trace grid, % of full occupancy (three calls share the chip)
+#endif
+#ifndef WF_TRACE_PATHS_PER_BLOCK
+#define WF_TRACE_PATHS_PER_BLOCK 2048 // > 0: trace grid <= paths / this (small multi-GPU shares)
+#endif
+
 // Wavefront buffers of one batch of n path slots, carved from `base`.
 static size_t wf_bytes(size_t n) {
     const size_t npad = (n + 255) / 256 * 256;
@@ -258,7 +265,13 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 256, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
-            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(c->trace_grid), dim3(WF_TRACE_BLOCK), 0, st, s, b,
+            // small batches (a rank's share of a multi-GPU frame) take a proportional part of
+            // the chip, so the calls in flight trace side by side instead of queueing
+            const size_t gmax = (size_t)c->trace_grid * WF_TRACE_GRID_PCT / 100;
+            const unsigned tgrid = WF_TRACE_PATHS_PER_BLOCK
+                ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, ((size_t)b.n + WF_TRACE_PATHS_PER_BLOCK - 1) / WF_TRACE_PATHS_PER_BLOCK))
+                : (unsigned)gmax;
+            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(tgrid), dim3(WF_TRACE_BLOCK), 0, st, s, b,
                                fp.mode);
         }
         HIPCHK(c, hipGetLastError());
