@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp
-for rep in ${REPS:-1}; do
+for rep in $(seq ${REPS:-1}); do
 for v in ${VARIANTS}; do
   PNRT_DEVICE_LIB=$PWD/pnraytracing_amd/variants/libpnrt_$v.so timeout -k 10 120 python bench.py --no-cpu-baseline \
     ${BENCH_ARGS} > gpurun_out/ab/$v.log 2>&1
