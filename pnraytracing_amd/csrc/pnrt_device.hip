@@ -370,9 +370,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     {
         ProfScope ps(c, PNRT_K_PRIMARY, w0);
-        const unsigned ptiles = PT_PRIM_TILE ? (unsigned)(((c->width + 15) / 16) * ((fp.rows + 15) / 16))
-                                             : (unsigned)((pix + 255) / 256);
-        hipLaunchKernelGGL(pt_primary_kernel, dim3(ptiles), dim3(256), 0, w0, s, fp, P.primary);
+        hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
     }
     HIPCHK(c, hipGetLastError());
     if (w1 != w0) {
@@ -581,7 +579,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     if (maxd >= PT_STACK - 1)
         return set_err(c, PNRT_E_SCENE, "BVH depth " + std::to_string(maxd) + " exceeds the kernel stack");
     // device numbering: breadth-first, so the top levels are the first indices
-    // (the trace kernel keeps nodes [0, WF_TREELET) in LDS); the visit order is
+    // (the top levels share cache lines); the visit order is
     // carried by the child refs and the axis, not by the numbering
     order.clear();
     if (fint(N[7]) != -1) order.push_back(0);

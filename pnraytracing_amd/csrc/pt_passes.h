@@ -15,9 +15,6 @@ PN_DEV f3 camera_dir(const FrameParams& fp, int px, int py) {
 }
 
 // ---- primary hits (once per call) ------------------------------------------------------------
-#ifndef PT_PRIM_TILE
-#define PT_PRIM_TILE 0       // primary pass: one workgroup per 16x16-pixel tile (measured slower) or 256 pixels of a row
-#endif
 #ifndef PT_PRIM_STK
 #define PT_PRIM_STK 8        // primary pass: stack entries per lane in LDS (deeper ones in private memory)
 #endif
@@ -85,20 +82,12 @@ PN_DEV bool traverse_closest_lds(const DevScene& s, const RayP& r, float& tMax, 
 
 // record: q0 = (P.xyz, bits(mat)), q1 = (N.xyz, u), q2 = (v, base.xyz); mat = -1 on a miss
 // (base = emissive of the hit material, or the env colour of the primary direction).
-// One workgroup per 16x16-pixel tile (coherent camera rays).
 __global__ void __launch_bounds__(256) pt_primary_kernel(DevScene s, FrameParams fp, float4* rec) {
     __shared__ uint2 lds[(PT_PRIM_STK > 0 ? PT_PRIM_STK : 1) * 256];
-#if PT_PRIM_TILE
-    const int tiles_x = (fp.width + 15) / 16;
-    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
-    const int px = tx * 16 + (threadIdx.x & 15), lr = ty * 16 + (threadIdx.x >> 4);
-    if (px >= fp.width || lr >= fp.rows) return;
-    const size_t i = (size_t)lr * fp.width + px;
-#else
+    // 256 pixels of a row per workgroup (16x16-pixel tiles measured slower)
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (size_t)fp.rows * fp.width) return;
     const int lr = (int)(i / fp.width), px = (int)(i - (size_t)lr * fp.width);
-#endif
     int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
     f3 eye = mk3(fp.eye[0], fp.eye[1], fp.eye[2]);
     f3 dir = camera_dir(fp, px, py);

@@ -28,9 +28,6 @@
 #define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
 #endif
 #define WF_LIGHT_SCAN PT_LIGHT_SCAN
-#ifndef WF_KO_P34
-#define WF_KO_P34 0         // timing diagnostic: light/env candidates not stored in the path state (wrong images)
-#endif
 #define WF_OVF 56
 #ifndef WF_QSHARDS
 #define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
@@ -263,7 +260,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     // stored as soon as final (shorter live ranges), and only when shade can use it:
     // shade takes (0, 0) for a path without a light ray, as the reference's
     // initial LDirect / lightPDF (:878-879)
-    if (!WF_KO_P34 && (nfl & WF_RLIGHT)) w.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);
+    if (nfl & WF_RLIGHT) w.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -279,7 +276,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
-    if (!WF_KO_P34 && (nfl & WF_RENV)) w.P4[i] = make_float4(LE.x, LE.y, LE.z, 0.f);
+    if (nfl & WF_RENV) w.P4[i] = make_float4(LE.x, LE.y, LE.z, 0.f);
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -344,16 +341,9 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
 #ifndef WF_SORT_OCTANT
 #define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
 #endif
-#ifndef WF_SORT_SUB
-#define WF_SORT_SUB 1      // direction bins per octant (1, or 3: + the dominant axis)
-#endif
-#define WF_NBIN (8 * WF_SORT_SUB)
+#define WF_NBIN 8
 PN_DEV int wf_dir_bin(const f3 d) {
-    const int oct = WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
-    if (WF_SORT_SUB == 1) return oct;
-    const float ax = pnm_fabs(d.x), ay = pnm_fabs(d.y), az = pnm_fabs(d.z);
-    const int dom = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
-    return oct * WF_SORT_SUB + dom;
+    return WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
 }
 PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays) {
     // Inside a segment the rays are grouped by direction bin: rays with the same
@@ -515,18 +505,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_STATS
 #define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
 #endif
-#ifndef WF_BUFFER_FETCH
-#define WF_BUFFER_FETCH 1   // the step's fetch as buffer loads with 32-bit offsets (one resource for nodes + tris)
-#endif
-#ifndef WF_Q3_SHARED
-#define WF_Q3_SHARED 1      // triangle lanes' unused fourth 16-B load goes to one shared address
-#endif
-#ifndef WF_TREELET
-#define WF_TREELET 0        // top nodes kept in LDS (0 = off; <= 160 at 6 waves/SIMD)
-#endif
-#ifndef WF_PF
-#define WF_PF 0             // request the next dequeue ticket one segment ahead
-#endif
 #ifndef WF_SUB
 #define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
 #endif
@@ -536,9 +514,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #endif
 #ifndef WF_TIMING
 #define WF_TIMING 0         // diagnostic builds: per-wave timestamps of the trace kernel
-#endif
-#ifndef WF_Q3_COND
-#define WF_Q3_COND 0        // node lanes only fetch the refs/axis quarter (triangle lanes skip it)
 #endif
 
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
@@ -576,20 +551,9 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
-#if WF_BUFFER_FETCH
+    // nodes and triangle records through one buffer resource (32-bit offsets)
     const __amdgpu_buffer_rsrc_t geo =
         __builtin_amdgcn_make_buffer_rsrc((void*)s.nodes, (short)0, (int)s.geo_bytes, 0x00020000);
-#endif
-#if WF_TREELET
-    // the top WF_TREELET nodes (breadth-first numbering: the first indices) in LDS:
-    // node fetches there bypass the vector L1 / texture-address path
-    __shared__ float4 tnodes[WF_TREELET * 4];
-    {
-        const int nt4 = 4 * (s.n_nodes < WF_TREELET ? s.n_nodes : WF_TREELET);
-        for (int k = threadIdx.x; k < nt4; k += WF_TRACE_BLOCK) tnodes[k] = s.nodes[k];
-        __syncthreads();
-    }
-#endif
     const int tl = threadIdx.x, lane = tl & 63;
     // rays are dequeued one queue segment at a time (<= 256 rays of one kind from
     // 256 neighbouring paths, kind-major); one atomic per segment
@@ -598,8 +562,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     uint32_t n_rays = 0;
     uint32_t next = 0, end = 0, ckind = 0, qpart = 0;
     bool exhausted = false;
-    uint32_t pf_t = 0;          // WF_PF: dequeue ticket in flight (lane 0's value)
-    bool pf_valid = false;
 
     RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
     float tMax = 0.f;
@@ -624,24 +586,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 for (;;) {
                     const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
                     uint32_t t = 0;
-                    if (WF_PF && pf_valid) {             // the ticket requested at the previous dequeue
-                        t = __builtin_amdgcn_readfirstlane(pf_t);
-                        pf_valid = false;
-                    } else {
-                        if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
-                        t = __builtin_amdgcn_readfirstlane(t);
-                    }
+                    if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
+                    t = __builtin_amdgcn_readfirstlane(t);
                     const uint32_t item = t * WF_QSHARDS + p;
                     if (item < nseg) { seg = item; break; }
                     if (++qpart == WF_QSHARDS) break;
-                }
-                if (WF_PF && seg < nseg) {
-                    // request the next ticket now: the atomic's latency passes while this
-                    // segment's rays are traced (its value is read at the next dequeue)
-                    const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
-                    pf_t = 0;
-                    if (lane == 0) pf_t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
-                    pf_valid = true;
                 }
                 if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
                 else {
@@ -714,32 +663,12 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     const bool isNode = !isTri & (cur != REF_NONE);
                     // ---- the step's single fetch: a triangle record or a node (lanes
                     // with neither re-read node 0, which stays in L1)
-#if WF_TREELET
-                    float4 q0, q1, q2, q3;
-                    if (!isTri & (!isNode | (cur < (uint32_t)WF_TREELET))) {     // treelet node (or node 0)
-                        const float4* ln = tnodes + 4 * (isNode ? cur : 0u);
-                        q0 = ln[0]; q1 = ln[1]; q2 = ln[2]; q3 = ln[3];
-                    } else {
-                        const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)cur;
-                        q0 = base[0]; q1 = base[1]; q2 = base[2]; q3 = base[3];
-                    }
-#else
-#if WF_BUFFER_FETCH
-                    // nodes and triangle records through one buffer resource, 32-bit offsets
                     const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)lt * 48u : (isNode ? cur : 0u) * 64u;
-                    // triangle lanes read the fourth quarter from one shared address (one
-                    // cache access per wave instead of one per lane)
+                    // triangle lanes read the unused fourth quarter from one shared address
+                    // (one cache access per wave instead of one per lane)
                     const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
                     const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
                                  q3 = geo_load(geo, off3);
-#else
-                    const float4* base = isTri ? s.tris + 3 * (size_t)lt : s.nodes + 4 * (size_t)(isNode ? cur : 0u);
-                    // WF_Q3_SHARED: triangle lanes read the fourth quarter from one shared
-                    // address (one cache access per wave instead of one per lane)
-                    const float4* b3 = (WF_Q3_SHARED && isTri) ? s.zero4 : base + 3;
-                    const float4 q0 = base[0], q1 = base[1], q2 = base[2], q3 = *b3;
-#endif
-#endif
                     // triangle test (:254-357 / :360-424)
                     float e0, e1, e2, det, ts;
                     const bool acc = tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts) & isTri;
@@ -835,12 +764,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     slot = meta & WF_META_SLOT;
     const bool useL = (meta & WF_META_RL) && !(oc & 0xffu);
     const bool useE = (meta & WF_META_RE) && !(oc >> 8);
-    float4 p3, p4;
-    if (WF_KO_P34) { p3 = make_float4(p2.x, 0.f, 0.f, 1.f); p4 = make_float4(p2.y, 0.f, 0.f, 1.f); }
-    else {
-        p3 = *(useL ? rd.P3 + i : s.zero4);
-        p4 = *(useE ? rd.P4 + i : s.zero4);
-    }
+    const float4 p3 = *(useL ? rd.P3 + i : s.zero4);
+    const float4 p4 = *(useE ? rd.P4 + i : s.zero4);
     // the continuation hit's records, in flight while the MIS sum waits for P3/P4
     // (a miss reads triangle 0's, unused)
     const HitFetch hf = hit_fetch(s, ht < 0 ? 0 : ht);
