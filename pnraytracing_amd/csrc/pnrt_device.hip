@@ -298,7 +298,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             unsigned long long stt[8];
             HIPCHK(c, hipStreamSynchronize(st));
             HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
-            fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu pop-only=%llu "
+            fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu uniform-fetch iters=%llu "
                     "refills=%llu rays=%llu  lane-steps/ray=%.1f  continuation lane-steps=%.1f%%\n", bounce, b.n, stt[0],
                     stt[0] ? (double)stt[1] / stt[0] : 0.0, stt[2], stt[3], stt[4], stt[5], stt[6],
                     stt[6] ? (double)stt[1] / stt[6] : 0.0, stt[1] ? 100.0 * stt[7] / stt[1] : 0.0);

@@ -650,8 +650,13 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     st[1] += __popcll(__ballot(busy != 0));
                     st[2] += __popcll(__ballot(busy != 0 && lc > 0));
                     st[3] += __popcll(__ballot(busy != 0 && lc <= 0 && cur != REF_NONE));
-                    st[4] += __popcll(__ballot(busy != 0 && lc <= 0 && cur == REF_NONE));
                     st[7] += __popcll(__ballot(busy != 0 && (rid >> 30) == 2u));     // continuation-ray lane steps
+                    {   // steps whose fetch address is the same for every active lane
+                        const uint64_t act = __ballot(busy != 0);
+                        const uint32_t fo = lc > 0 ? 0x80000000u + (uint32_t)lt : cur;
+                        const uint32_t f0 = __shfl(fo, act ? __ffsll((long long)act) - 1 : 0);
+                        st[4] += (act != 0 && __ballot(busy != 0 && fo != f0) == 0) ? 1 : 0;
+                    }
                 }
                 if (busy) {
                     // One step, written branch-light: the triangle test and the node
