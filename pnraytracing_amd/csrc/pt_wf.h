@@ -433,10 +433,6 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
-// Per-lane spill area of the traversal stack (address formed only when used).
-PN_DEV uint2* wf_ovf(const WfBufs& b, int tl) {
-    return b.ovf + ((size_t)blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride;
-}
 // Leaf ref -> triangle range; the leaf-table lookup is behind a scene-uniform
 // (scalar) branch, so scenes without table leaves pay no divergent branch.
 PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& cnt) {
@@ -451,27 +447,38 @@ PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& c
     }
 }
 
-template <int STK>
-PN_DEV void wf_push(uint2* lds, uint2* ovf, int lane, int& sp, uint32_t ref, float z) {
-    uint2 e = make_uint2(ref, __float_as_uint(z));
-    if (sp < STK) lds[sp * WF_TRACE_BLOCK + lane] = e;
-    else ovf[sp - STK] = e;
-    ++sp;
+// The lane's stack position is one register: spa = sp * 2048 + 8 * tl, the LDS
+// byte address of entry sp of lane tl (entries of one depth are 2048 B apart,
+// 256 lanes x 8 B), so sp = spa >> 11 and the lane's slot is spa & 2047 -- no
+// separate per-lane base register (at 8 waves/SIMD the compiler spilled it).
+// Entries deeper than STK go to the global spill area, addressed from the same
+// value through one block-uniform buffer resource.
+PN_DEV uint32_t wf_ovf_off(const WfBufs& b, uint32_t spa, int stk) {
+    const uint32_t tl = (spa & 2047u) >> 3, k = (spa >> 11) - (uint32_t)stk;
+    return ((blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride + k) * 8u;
 }
 template <int STK>
-PN_DEV uint2 wf_pop(const uint2* lds, const uint2* ovf, int lane, int& sp) {
-    --sp;
+PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, uint32_t ref, float z) {
+    const uint2 e = make_uint2(ref, __float_as_uint(z));
+    if (spa < STK * 2048u) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + spa) = e;
+    else b.ovf[wf_ovf_off(b, spa, STK) / 8u] = e;
+    spa += 2048u;
+}
+template <int STK>
+PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa) {
+    spa -= 2048u;
     // the common case is a ds_read; the rare spill read is a buffer load, which the
     // compiler cannot merge with the LDS read into one flat load (a flat load waits
     // for every outstanding vector-memory operation, stores included)
     uint2 e;
-    if (sp >= STK) {
+    if (spa >= STK * 2048u) {
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)ovf, (short)0, 0x7fffffff, 0x00020000);
-        e.x = __builtin_amdgcn_raw_buffer_load_b32(rs, (sp - STK) * 8, 0, 0);
-        e.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (sp - STK) * 8 + 4, 0, 0);
+            __builtin_amdgcn_make_buffer_rsrc((void*)b.ovf, (short)0, 0x7fffffff, 0x00020000);
+        const uint32_t off = wf_ovf_off(b, spa, STK);
+        e.x = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+        e.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off + 4, 0, 0);
     } else {
-        e = lds[sp * WF_TRACE_BLOCK + lane];
+        e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + spa);
     }
     return e;
 }
@@ -541,7 +548,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 // wave-level decision (ballot) at a reconvergence point: the ray <-> lane
 // refill runs between traversal phases.
 #ifndef WF_TRACE_WAVES
-#define WF_TRACE_WAVES 7      // waves per SIMD (72 VGPRs, built without SLP packing; 3 spilled values)
+#define WF_TRACE_WAVES 8      // waves per SIMD (64 VGPRs: no SLP packing, one-register stack position)
 #endif
 PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -565,7 +572,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 
     RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
     float tMax = 0.f;
-    int hitTri = -1, lt = 0, lc = 0, sp = 0;
+    int hitTri = -1, lt = 0, lc = 0;
+    uint32_t spa = (uint32_t)threadIdx.x * 8u;      // stack position (see wf_push)
     uint32_t cur = REF_NONE, rid = 0;
     bool any = true;
     int busy = 0;
@@ -627,7 +635,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
                     r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
-                    hitTri = -1; sp = 0; cur = root; lt = nlt; lc = nlc;
+                    hitTri = -1; spa &= 2047u; cur = root; lt = nlt; lc = nlc;
                     busy = 1;
                 }
             }
@@ -696,7 +704,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
                     const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
                     const float zFar = rightFirst ? zloL : zloR;
-                    if (hNear & hFar) wf_push<STK>(lds, wf_ovf(b, tl), tl, sp, farRef, zFar);
+                    if (hNear & hFar) wf_push<STK>(lds, b, spa, farRef, zFar);
                     const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
                     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
                     int gs, gc;
@@ -706,9 +714,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     cur = isNode ? (goLeaf ? REF_NONE : go) : cur;
                     // ---- next fetch target: pop when nothing is pending
                     const bool idle = !done & (lc <= 0) & (cur == REF_NONE);
-                    done = done | (idle & (sp == 0));
-                    if (idle & (sp > 0)) {
-                        const uint2 e = wf_pop<STK>(lds, wf_ovf(b, tl), tl, sp);
+                    done = done | (idle & (spa < 2048u));
+                    if (idle & (spa >= 2048u)) {
+                        const uint2 e = wf_pop<STK>(lds, b, spa);
                         const float z = __uint_as_float(e.y);
                         const bool culled = cull & (z > tMax * 1.000001f) & (z > 1e-20f);
                         const bool eLeaf = (e.x & REF_LEAF) != 0u;
