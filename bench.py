@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-image", default="")
     ap.add_argument("--spp", type=int, default=0, help="experiment: samples per step other than the config's 4")
+    ap.add_argument("--kernel-times", action="store_true",
+                    help="time every kernel class with HIP events (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     return ap.parse_args()
@@ -122,7 +124,10 @@ def main():
     W, H, spp = cfg.width, cfg.height, cfg.spp
 
     pt = PathTracer(local)
-    stream = torch.cuda.Stream()               # a real stream handle (the default one is NULL)
+    # torch works on the library's own stream (created with the context, before its
+    # three worker streams): a fifth stream of torch's own would share one of the
+    # process's 4 hardware queues with a busy stream (measured -4 %)
+    stream = torch.cuda.ExternalStream(pt.stream_handle())
     torch.cuda.set_stream(stream)
     pt.set_stream(stream.cuda_stream)
     opts = (TRAVERSE_ZCULL if args.mode == "zcull" else TRAVERSE_EXACT) | {"v1": KERNEL_V1, "v3": 0}[args.kernel]
@@ -148,6 +153,9 @@ def main():
     torch.cuda.synchronize()
     # live per-kernel timing: the library brackets every launch with HIP events
     # recorded on the stream it launches on (pnrt_profile_enable)
+    # only the dominant kernel is bracketed unless --kernel-times: every event record
+    # is a queue packet between launches of the overlapped calls
+    pt.profile_select(None if args.kernel_times else [{"v1": "v1", "v3": "trace"}[args.kernel]])
     pt.profile_enable(True)
     t0 = time.perf_counter()
     for k in range(args.steps):

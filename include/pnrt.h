@@ -59,6 +59,9 @@ void pnrt_destroy(pnrt_ctx* ctx);
 const char* pnrt_last_error(pnrt_ctx* ctx);
 /* Launch work on `hip_stream` (a hipStream_t; NULL = the context's stream). */
 int pnrt_set_stream(pnrt_ctx* ctx, void* hip_stream);
+/* The context's own stream (created with it, before its worker streams): a caller
+ * that wraps it (e.g. torch.cuda.ExternalStream) adds no stream of its own. */
+void* pnrt_get_stream(pnrt_ctx* ctx);
 
 /* Replaces the five TBO/texture uploads main.cpp:409-524 (texture units 0-4)
  * and the lightsSize/lightsSumArea uniforms (main.cpp:391-392):
@@ -141,6 +144,10 @@ typedef struct {
 } pnrt_profile;
 int pnrt_profile_enable(pnrt_ctx* ctx, int on);
 int pnrt_profile_read(pnrt_ctx* ctx, pnrt_profile* out);
+/* Kernel classes bracketed while profiling is enabled: bit k = PNRT_K_k (default
+ * all).  Timing only the dominant class keeps the event records off the other
+ * launches (each record is a queue packet between kernels). */
+int pnrt_profile_select(pnrt_ctx* ctx, int class_mask);
 
 /* GPU BuildBVH: the reference's binned-SAH build
  * (include/BVH.hpp:92-173, called from the BVH ctor :16-19 via main.cpp's

@@ -143,6 +143,8 @@ def _type_device(lib):
     _sig(lib, "pnrt_get_device_info", INT, P, ctypes.POINTER(DeviceInfo))
     _sig(lib, "pnrt_debug_math", INT, P, INT, F, F, F, INT)
     _sig(lib, "pnrt_profile_enable", INT, P, INT)
+    _sig(lib, "pnrt_profile_select", INT, P, INT)
+    _sig(lib, "pnrt_get_stream", P, P)
     _sig(lib, "pnrt_upload_env_build", INT, P, F, INT, INT)
     _sig(lib, "pnrt_read_env_table", INT, P, F)
     _sig(lib, "pnrt_profile_read", INT, P, ctypes.POINTER(Profile))

@@ -104,6 +104,7 @@ struct pnrt_ctx {
     int wf_stack_need = 0;                 // wide-traversal stack entries per lane (from upload)
     // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
     bool prof_on = false;
+    int prof_mask = -1;     // kernel classes bracketed while profiling (pnrt_profile_select)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
     double prof_ms[PNRT_K_COUNT] = {};
@@ -140,7 +141,7 @@ static hipEvent_t ev_get(pnrt_ctx* c) {
 struct ProfScope {     // records on the launch stream, so it times exactly that stream's launches
     pnrt_ctx* c; int k; hipStream_t st; hipEvent_t a = nullptr;
     ProfScope(pnrt_ctx* c_, int k_, hipStream_t st_ = nullptr) : c(c_), k(k_), st(st_ ? st_ : c_->stream) {
-        if (c->prof_on && (a = ev_get(c))) (void)hipEventRecord(a, st);
+        if (c->prof_on && ((c->prof_mask >> k) & 1) && (a = ev_get(c))) (void)hipEventRecord(a, st);
     }
     ~ProfScope() {
         if (!a) return;
@@ -483,6 +484,8 @@ void pnrt_destroy(pnrt_ctx* c) {
 }
 
 const char* pnrt_last_error(pnrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* pnrt_get_stream(pnrt_ctx* c) { return c ? static_cast<void*>(c->own_stream) : nullptr; }
 
 int pnrt_set_stream(pnrt_ctx* c, void* s) {
     if (!c) return PNRT_E_ARG;
@@ -874,6 +877,12 @@ int pnrt_profile_enable(pnrt_ctx* c, int on) {
     if (rc) return rc;
     c->prof_on = on != 0;
     for (int k = 0; k < PNRT_K_COUNT; ++k) { c->prof_ms[k] = 0.0; c->prof_n[k] = 0; }
+    return PNRT_OK;
+}
+
+int pnrt_profile_select(pnrt_ctx* c, int mask) {
+    if (!c) return PNRT_E_ARG;
+    c->prof_mask = mask;
     return PNRT_OK;
 }
 

@@ -43,6 +43,22 @@ class ShardedFrame:
         # of the multi-GPU path on one GPU / CPU-only hosts); RCCL gathers in HBM
         self.stage = (dist.is_initialized() and self.device.type == "cuda"
                       and dist.get_backend(group) == "gloo")
+        # the tracer and this object's torch work (pack buffers, collectives, image
+        # assembly) share one stream: the caller's current stream, or -- when that is
+        # the NULL stream, which does not order against the tracer's non-blocking
+        # streams -- the tracer's own stream, wrapped for torch
+        self.stream = None
+        if self.device.type == "cuda" and hasattr(tracer, "set_stream"):
+            cur = torch.cuda.current_stream(self.device)
+            if cur.cuda_stream == 0 and hasattr(tracer, "stream_handle"):
+                self.stream = torch.cuda.ExternalStream(tracer.stream_handle(), device=self.device)
+                tracer.set_stream(None)
+            else:
+                tracer.set_stream(cur.cuda_stream)
+        self._on_stream(lambda: self._alloc(H, W))
+
+    def _alloc(self, H: int, W: int):
+        band = self.band
         rows = [shard_rows(H, band, self.world, r) for r in range(self.world)]
         self.rows = [torch.as_tensor(r, device=self.device) for r in rows]
         self.my_rows = len(rows[self.rank])
@@ -60,14 +76,12 @@ class ShardedFrame:
         self._last = None
         self._newest = 0
         self.image = torch.zeros((H, W, 4), dtype=torch.float32, device=self.device) if self.rank == 0 else None
-        if self.device.type == "cuda" and hasattr(tracer, "set_stream"):
-            tracer.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def render(self, first_frame: int, n_frames: int):
         """Asynchronously render frames first..first+n-1 of this rank's rows."""
         self.tracer.render(first_frame, n_frames, self.band, self.world, self.rank)
 
-    def gather(self) -> torch.Tensor | None:
+    def _gather(self) -> torch.Tensor | None:
         """Pack this rank's rows, gather on rank 0; returns the H x W x 4 image
         (row 0 = bottom) on rank 0 and None elsewhere."""
         if self.my_rows:
@@ -81,6 +95,25 @@ class ShardedFrame:
             return None
         return self._assemble(self.recv)
 
+    def _on_stream(self, fn):
+        if self.stream is None:
+            return fn()
+        with torch.cuda.stream(self.stream):
+            return fn()
+
+    def gather(self) -> torch.Tensor | None:
+        """Pack this rank's rows, gather on rank 0; returns the H x W x 4 image
+        (row 0 = bottom) on rank 0 and None elsewhere."""
+        return self._on_stream(self._gather)
+
+    def gather_async(self) -> None:
+        """Start the gather of the current frame (see _gather_async)."""
+        return self._on_stream(self._gather_async)
+
+    def finish(self) -> torch.Tensor | None:
+        """Complete the outstanding gathers; rank 0 gets the newest frame's image."""
+        return self._on_stream(self._finish)
+
     def _assemble(self, recv) -> torch.Tensor:
         for r in range(self.world):
             n = len(self.rows[r])
@@ -88,13 +121,13 @@ class ShardedFrame:
                 self.image.index_copy_(0, self.rows[r], recv[r][:n].to(self.device, non_blocking=False))
         return self.image
 
-    def gather_async(self) -> None:
+    def _gather_async(self) -> None:
         """Pack this rank's rows and START the gather (RCCL) without making the
         render stream wait for it: the next frames render while the rows travel
         over xGMI.  Double-buffered; :meth:`finish` completes the last gather and
         assembles the image on rank 0.  (Synchronous for one rank / gloo staging.)"""
         if self.world == 1 or self.stage:
-            self._last = self.gather()
+            self._last = self._gather()
             return
         slot = self._slot
         self._slot ^= 1
@@ -107,7 +140,7 @@ class ShardedFrame:
                                        group=self.group, async_op=True)
         self._newest = slot
 
-    def finish(self) -> torch.Tensor | None:
+    def _finish(self) -> torch.Tensor | None:
         """Complete the outstanding gathers; rank 0 gets the newest frame's image."""
         if self.world == 1 or self.stage:
             return self._last

@@ -107,6 +107,10 @@ class PathTracer:
     def set_options(self, traverse_mode: int):
         self._ck(self._lib.pnrt_set_options(self._ctx, traverse_mode), "pnrt_set_options")
 
+    def stream_handle(self) -> int:
+        """The context's own hipStream_t (for torch.cuda.ExternalStream)."""
+        return int(self._lib.pnrt_get_stream(self._ctx) or 0)
+
     def set_stream(self, stream_handle: int | None):
         self._ck(self._lib.pnrt_set_stream(self._ctx, ctypes.c_void_p(stream_handle or 0)), "pnrt_set_stream")
 
@@ -148,6 +152,11 @@ class PathTracer:
     def profile_enable(self, on: bool = True):
         """Bracket every kernel launch with HIP events on the launch stream (resets totals)."""
         self._ck(self._lib.pnrt_profile_enable(self._ctx, int(bool(on))), "pnrt_profile_enable")
+
+    def profile_select(self, classes=None):
+        """Kernel classes to time (names of K_CLASSES; None = all)."""
+        mask = -1 if classes is None else sum(1 << N.K_CLASSES.index(k) for k in classes)
+        self._ck(self._lib.pnrt_profile_select(self._ctx, mask), "pnrt_profile_select")
 
     def profile_read(self) -> dict:
         """{kernel class: (total ms, launches)} since profile_enable (synchronises)."""
