@@ -93,6 +93,10 @@ def stored(path, cfg_name):
 
 def main():
     args = parse()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # multi-rank: RCCL adds a stream of its own beside the library's four (own +
+        # three workers); 8 hardware queues keep it off theirs (set before HIP starts)
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     import torch
     import torch.distributed as dist
 
