@@ -19,7 +19,7 @@
 #define WF_STACK 8          // LDS stack entries per lane; deeper spills to global
 #endif
 #ifndef WF_REFILL_PCT
-#define WF_REFILL_PCT 65    // refill a wave when at most this % of its lanes still trace
+#define WF_REFILL_PCT 40    // refill a wave when at most this % of its lanes still trace (tuned at 8 waves)
 #endif
 #ifndef WF_PIPES
 #define WF_PIPES 3          // pnrt_render calls in flight (buffer sets / worker streams; + the context stream = 4 HW queues)
