@@ -247,6 +247,16 @@ static WfLayout wf_layout(char* base, size_t n) {
     return L;
 }
 
+// Trace grid for a batch of n paths: small batches (a rank's share of a
+// multi-GPU frame) take a proportional part of the chip, and no launch more than
+// WF_TRACE_GRID_PCT %, so the calls in flight trace side by side instead of queueing.
+static unsigned trace_grid_for(const pnrt_ctx* c, size_t n) {
+    const size_t gmax = (size_t)c->trace_grid * WF_TRACE_GRID_PCT / 100;
+    return WF_TRACE_PATHS_PER_BLOCK
+               ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + WF_TRACE_PATHS_PER_BLOCK - 1) / WF_TRACE_PATHS_PER_BLOCK))
+               : (unsigned)gmax;
+}
+
 // One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
 // its colours land in frame slots [0, cf) of `colors`.
 static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, const WfLayout& L, hipStream_t st,
@@ -266,13 +276,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 256, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
-            // small batches (a rank's share of a multi-GPU frame) take a proportional part of
-            // the chip, so the calls in flight trace side by side instead of queueing
-            const size_t gmax = (size_t)c->trace_grid * WF_TRACE_GRID_PCT / 100;
-            const unsigned tgrid = WF_TRACE_PATHS_PER_BLOCK
-                ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, ((size_t)b.n + WF_TRACE_PATHS_PER_BLOCK - 1) / WF_TRACE_PATHS_PER_BLOCK))
-                : (unsigned)gmax;
-            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(tgrid), dim3(WF_TRACE_BLOCK), 0, st, s, b,
+            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(trace_grid_for(c, b.n)), dim3(WF_TRACE_BLOCK), 0, st, s, b,
                                fp.mode);
         }
         HIPCHK(c, hipGetLastError());

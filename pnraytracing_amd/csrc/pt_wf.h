@@ -523,6 +523,88 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #define WF_TIMING 0         // diagnostic builds: per-wave timestamps of the trace kernel
 #endif
 
+PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// One lane's traversal state (a ray being traced).
+struct TravState {
+    RayP r;
+    float tMax;
+    int hitTri, lt, lc;       // accepted triangle; pending triangle range [lt, lt + lc)
+    uint32_t spa, cur;        // stack position (see wf_push); node to visit next
+    bool any;                 // any-hit (shadow) ray
+};
+
+// One traversal step of a lane's ray; returns true when the ray is finished
+// (an any-hit ray accepted a triangle, or nothing is left to visit).
+template <int STK, bool ID>
+PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo,
+                                                   uint2* lds, TravState& t) {
+    // One step, written branch-light: the triangle test and the node
+    // visit are both evaluated (a wave almost always holds lanes of
+    // both kinds, so both paths ran anyway) and their results are
+    // selected per lane; only memory side effects (stack push/pop,
+    // the result store) and the rare IEEE division stay in branches.
+    const bool isTri = t.lc > 0;
+    const bool isNode = !isTri & (t.cur != REF_NONE);
+    // ---- the step's single fetch: a triangle record or a node (lanes
+    // with neither re-read node 0, which stays in L1)
+    const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)t.lt * 48u : (isNode ? t.cur : 0u) * 64u;
+    // triangle lanes read the unused fourth quarter from one shared address
+    // (one cache access per wave instead of one per lane)
+    const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
+    const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
+                 q3 = geo_load(geo, off3);
+    // triangle test (:254-357 / :360-424)
+    float e0, e1, e2, det, ts;
+    const bool acc = tri_test<ID>(t.r, q0, q1, q2, t.tMax, e0, e1, e2, det, ts) & isTri;
+    t.hitTri = acc ? t.lt : t.hitTri;
+    bool done = acc & t.any;
+    if (acc & !t.any) t.tMax = ts * (1.0f / det);
+    t.lt += isTri ? 1 : 0;
+    t.lc -= isTri ? 1 : 0;
+    // node visit: both child boxes (:447-457), z-slab culling
+    const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
+                               __float_as_uint(q3.w));
+    const float tmc = t.tMax * 1.000001f;
+    float zloL, zloR;
+    bool hL = box_fast<ID>(t.r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+    bool hR = box_fast<ID>(t.r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
+    const bool cull = t.r.cull_ok();
+    hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
+    hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
+    const bool rightFirst = comp(t.r.d, (int)(m.z & 3u)) < 0;     // :448
+    const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+    const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
+    const float zFar = rightFirst ? zloL : zloR;
+    if (hNear & hFar) wf_push<STK>(lds, b, t.spa, farRef, zFar);
+    const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
+    const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
+    int gs, gc;
+    decode_leaf_fast(s, go, gs, gc);
+    t.lt = goLeaf ? gs : t.lt;
+    t.lc = goLeaf ? gc : t.lc;
+    t.cur = isNode ? (goLeaf ? REF_NONE : go) : t.cur;
+    // ---- next fetch target: pop when nothing is pending
+    const bool idle = !done & (t.lc <= 0) & (t.cur == REF_NONE);
+    done = done | (idle & (t.spa < 2048u));
+    if (idle & (t.spa >= 2048u)) {
+        const uint2 e = wf_pop<STK>(lds, b, t.spa);
+        const float z = __uint_as_float(e.y);
+        const bool culled = cull & (z > t.tMax * 1.000001f) & (z > 1e-20f);
+        const bool eLeaf = (e.x & REF_LEAF) != 0u;
+        int es, ec;
+        decode_leaf_fast(s, e.x, es, ec);
+        t.lt = (!culled & eLeaf) ? es : t.lt;
+        t.lc = (!culled & eLeaf) ? ec : t.lc;
+        t.cur = (!culled & !eLeaf) ? e.x : t.cur;
+    }
+    return done;
+}
+
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
                         uint32_t& p) {
@@ -550,11 +632,6 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 8      // waves per SIMD (64 VGPRs: no SLP packing, one-register stack position)
 #endif
-PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
@@ -570,12 +647,14 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     uint32_t next = 0, end = 0, ckind = 0, qpart = 0;
     bool exhausted = false;
 
-    RayP r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
-    float tMax = 0.f;
-    int hitTri = -1, lt = 0, lc = 0;
-    uint32_t spa = (uint32_t)threadIdx.x * 8u;      // stack position (see wf_push)
-    uint32_t cur = REF_NONE, rid = 0;
-    bool any = true;
+    TravState t;
+    t.r = make_ray(mk3(0.f, 0.f, 0.f), mk3(0.f, 0.f, 1.f), 0);
+    t.tMax = 0.f;
+    t.hitTri = -1; t.lt = 0; t.lc = 0;
+    t.spa = (uint32_t)threadIdx.x * 8u;      // stack position (see wf_push)
+    t.cur = REF_NONE;
+    t.any = true;
+    uint32_t rid = 0;
     int busy = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
 
@@ -634,8 +713,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         root = s.root_ref;
                         if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
-                    r = nr; tMax = ntmax; any = nany; rid = (kind << 30) | p;
-                    hitTri = -1; spa &= 2047u; cur = root; lt = nlt; lc = nlc;
+                    t.r = nr; t.tMax = ntmax; t.any = nany; rid = (kind << 30) | p;
+                    t.hitTri = -1; t.spa &= 2047u; t.cur = root; t.lt = nlt; t.lc = nlc;
                     busy = 1;
                 }
             }
@@ -656,97 +735,39 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 if (WF_STATS) {
                     st[0] += 1;
                     st[1] += __popcll(__ballot(busy != 0));
-                    st[2] += __popcll(__ballot(busy != 0 && lc > 0));
-                    st[3] += __popcll(__ballot(busy != 0 && lc <= 0 && cur != REF_NONE));
+                    st[2] += __popcll(__ballot(busy != 0 && t.lc > 0));
+                    st[3] += __popcll(__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE));
                     st[7] += __popcll(__ballot(busy != 0 && (rid >> 30) == 2u));     // continuation-ray lane steps
                     {   // steps whose fetch address is the same for every active lane
                         const uint64_t act = __ballot(busy != 0);
-                        const uint32_t fo = lc > 0 ? 0x80000000u + (uint32_t)lt : cur;
+                        const uint32_t fo = t.lc > 0 ? 0x80000000u + (uint32_t)t.lt : t.cur;
                         const uint32_t f0 = __shfl(fo, act ? __ffsll((long long)act) - 1 : 0);
                         st[4] += (act != 0 && __ballot(busy != 0 && fo != f0) == 0) ? 1 : 0;
                     }
                 }
                 if (busy) {
-                    // One step, written branch-light: the triangle test and the node
-                    // visit are both evaluated (a wave almost always holds lanes of
-                    // both kinds, so both paths ran anyway) and their results are
-                    // selected per lane; only memory side effects (stack push/pop,
-                    // the result store) and the rare IEEE division stay in branches.
-                    const bool isTri = lc > 0;
-                    const bool isNode = !isTri & (cur != REF_NONE);
-                    // ---- the step's single fetch: a triangle record or a node (lanes
-                    // with neither re-read node 0, which stays in L1)
-                    const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)lt * 48u : (isNode ? cur : 0u) * 64u;
-                    // triangle lanes read the unused fourth quarter from one shared address
-                    // (one cache access per wave instead of one per lane)
-                    const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
-                    const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
-                                 q3 = geo_load(geo, off3);
-                    // triangle test (:254-357 / :360-424)
-                    float e0, e1, e2, det, ts;
-                    const bool acc = tri_test<ID>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts) & isTri;
-                    hitTri = acc ? lt : hitTri;
-                    bool done = acc & any;
-                    if (acc & !any) tMax = ts * (1.0f / det);
-                    lt += isTri ? 1 : 0;
-                    lc -= isTri ? 1 : 0;
-                    // node visit: both child boxes (:447-457), z-slab culling
-                    const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
-                                               __float_as_uint(q3.w));
-                    const float tmc = tMax * 1.000001f;
-                    float zloL, zloR;
-                    bool hL = box_fast<ID>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
-                    bool hR = box_fast<ID>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
-                    const bool cull = r.cull_ok();
-                    hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
-                    hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
-                    const bool rightFirst = comp(r.d, (int)(m.z & 3u)) < 0;     // :448
-                    const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
-                    const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
-                    const float zFar = rightFirst ? zloL : zloR;
-                    if (hNear & hFar) wf_push<STK>(lds, b, spa, farRef, zFar);
-                    const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
-                    const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
-                    int gs, gc;
-                    decode_leaf_fast(s, go, gs, gc);
-                    lt = goLeaf ? gs : lt;
-                    lc = goLeaf ? gc : lc;
-                    cur = isNode ? (goLeaf ? REF_NONE : go) : cur;
-                    // ---- next fetch target: pop when nothing is pending
-                    const bool idle = !done & (lc <= 0) & (cur == REF_NONE);
-                    done = done | (idle & (spa < 2048u));
-                    if (idle & (spa >= 2048u)) {
-                        const uint2 e = wf_pop<STK>(lds, b, spa);
-                        const float z = __uint_as_float(e.y);
-                        const bool culled = cull & (z > tMax * 1.000001f) & (z > 1e-20f);
-                        const bool eLeaf = (e.x & REF_LEAF) != 0u;
-                        int es, ec;
-                        decode_leaf_fast(s, e.x, es, ec);
-                        lt = (!culled & eLeaf) ? es : lt;
-                        lc = (!culled & eLeaf) ? ec : lc;
-                        cur = (!culled & !eLeaf) ? e.x : cur;
-                    }
+                    const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
                     if (done) {
                         const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
                         if (!WF_DIAG_NOSTORE) {
-                            if (kind == 2) b.hit[p] = hitTri;
-                            else b.occ[2 * (size_t)p + kind] = hitTri >= 0 ? 1 : 0;
+                            if (kind == 2) b.hit[p] = t.hitTri;
+                            else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
                         }
                         busy = 0;
                     }
                 }
 #if WF_DIAG_VALU
                 {   // timing diagnostic: extra VALU per iteration (is the loop issue-bound?)
-                    float d = __int_as_float(lt);
+                    float d = __int_as_float(t.lt);
 #pragma unroll
                     for (int q = 0; q < WF_DIAG_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
-                    lt = __float_as_int(d) == 0x7fffffff ? 0 : lt;
+                    t.lt = __float_as_int(d) == 0x7fffffff ? 0 : t.lt;
                 }
 #endif
                 if (__popcll(__ballot(busy != 0)) <= thr) break;
             }
         };
-        if (__ballot(busy != 0 && r.kz() != 2) == 0) run(std::true_type{});
+        if (__ballot(busy != 0 && t.r.kz() != 2) == 0) run(std::true_type{});
         else run(std::false_type{});
     }
     if (WF_TIMING && lane == 0) {      // diagnostic builds: per-wave start / queue-empty / end (100 MHz clock)
