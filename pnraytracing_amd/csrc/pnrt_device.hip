@@ -237,8 +237,10 @@ static WfLayout wf_layout(char* base, size_t n) {
     off = (off + 255) & ~(size_t)255;
     b.npad = (uint32_t)((n + 255) / 256 * 256);
     b.nseg_k = b.npad / 256;
-    b.rayO = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
-    b.rayD = reinterpret_cast<float4*>(base + off); off += (size_t)b.npad * 48;
+    // ray records of the queued kinds (light, env; + continuation without WF_CONT_FROM_STATE)
+    const size_t rec = (size_t)b.npad * 16 * (WF_CONT_FROM_STATE ? 2 : 3);
+    b.rayO = reinterpret_cast<float4*>(base + off); off += rec;
+    b.rayD = reinterpret_cast<float4*>(base + off); off += rec;
     b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
     off = (off + 255) & ~(size_t)255;
     b.counter = reinterpret_cast<unsigned int*>(base + off);               // 8 counters, 256 B apart

@@ -341,11 +341,21 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
 #ifndef WF_SORT_OCTANT
 #define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
 #endif
+#ifndef WF_CONT_FROM_STATE
+#define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued
+#endif
 #define WF_NBIN 8
 PN_DEV int wf_dir_bin(const f3 d) {
     return WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
 }
-PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays) {
+//
+// Continuation rays (WF_CONT_FROM_STATE): every live path has one and the setup
+// has just compacted the block's live paths to entries [256 j, 256 j + total),
+// so their segment IS that range of the path state -- origin P0.xyz, direction
+// P1.xyz, the same floats a ray record would copy.  Only the count is stored
+// (sorting them by octant measured neutral, 2 x 3 runs).
+PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays, uint32_t total) {
+    constexpr int NK = WF_CONT_FROM_STATE ? 2 : 3;     // kinds with queued ray records
     // Inside a segment the rays are grouped by direction bin: rays with the same
     // signs take the same near/far choice at every node (:448), so a wave walks
     // the tree more coherently.  Slots within a bin come from LDS atomics (order
@@ -357,13 +367,14 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
     int oct[3];
     unsigned int rank[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < NK; ++k) {
         const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
         oct[k] = wf_dir_bin(d);
         rank[k] = (nfl & need[k]) ? atomicAdd(&bin[k][oct[k]], 1u) : 0u;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {                    // exclusive prefix over the bins of a kind
+    if (NK == 2 && threadIdx.x == 2) b.segcount[2 * b.nseg_k + blockIdx.x] = total;
+    if (threadIdx.x < NK) {                   // exclusive prefix over the bins of a kind
         unsigned int run = 0;
         for (int o = 0; o < WF_NBIN; ++o) { const unsigned int c = bin[threadIdx.x][o]; bin[threadIdx.x][o] = run; run += c; }
         bin[threadIdx.x][WF_NBIN] = run;
@@ -371,7 +382,7 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < NK; ++k) {
         if (nfl & need[k]) {
             const size_t slot = (size_t)k * b.npad + (size_t)blockIdx.x * 256 + bin[k][oct[k]] + rank[k];
             const f3 o = k == 1 ? rays.oP : rays.oOff;
@@ -429,7 +440,7 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
     BounceRays rays;
     if (cont) nfl = wf_setup_core<WF_GEN_EARLY>(s, fp, b, j, i, 0, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
-    wf_enqueue(b, j, nfl, rays);     // every lane of the wave reaches this point
+    wf_enqueue(b, j, nfl, rays, total);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
@@ -608,8 +619,11 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
                         uint32_t& p) {
-    const float4 ro = b.rayO[slot], rd = b.rayD[slot];
-    p = __float_as_uint(ro.w);
+    // continuation rays: path entry = slot - 2 npad, read from the state the setup wrote
+    const bool fromState = WF_CONT_FROM_STATE && kind == 2;     // wave-uniform
+    const uint32_t e = fromState ? slot - 2u * b.npad : slot;
+    const float4 ro = (fromState ? b.wr.P0 : b.rayO)[e], rd = (fromState ? b.wr.P1 : b.rayD)[e];
+    p = fromState ? e : __float_as_uint(ro.w);
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
     r = make_ray(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), mode);
@@ -870,5 +884,5 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     BounceRays rays;
     if (cont) nfl = wf_setup_core<WF_SHADE_EARLY>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
-    wf_enqueue(b, j, nfl, rays);     // every lane of the wave reaches this point
+    wf_enqueue(b, j, nfl, rays, total);     // every lane of the wave reaches this point
 }
