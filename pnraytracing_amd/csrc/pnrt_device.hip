@@ -70,6 +70,8 @@ struct pnrt_ctx {
     // env + textures
     void* hdr = nullptr;
     void* rnd = nullptr;
+    void* hdr_q = nullptr;      // footprint records of both (DevScene::hdr_q)
+    void* rnd_q = nullptr;
     void* tex[PT_MAX_TEXTURES] = {};
     int tex_w[PT_MAX_TEXTURES] = {}, tex_h[PT_MAX_TEXTURES] = {};
     float* unorm8 = nullptr;
@@ -424,6 +426,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     return PNRT_OK;
 }
 
+static void free_env(pnrt_ctx* c);
+
 extern "C" {
 
 const char* pnrt_version(void) { return "pnrt-mi355x 0.1 (gfx950)"; }
@@ -469,7 +473,7 @@ void pnrt_destroy(pnrt_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)sync_all(c);
     free_scene(c);
-    (void)hipFree(c->hdr); (void)hipFree(c->rnd);
+    free_env(c);
     for (void* t : c->tex) (void)hipFree(t);
     (void)hipFree(c->unorm8);
     (void)hipFree(c->accum);
@@ -726,12 +730,44 @@ int pnrt_upload_texture(pnrt_ctx* c, int slot, const uint8_t* px, int w, int h, 
     return PNRT_OK;
 }
 
+// Footprint records (DevScene::hdr_q / rnd_q) of a w x h image: record (qj, qi)
+// = texels (bottom, left), (bottom, right), (top, left), (top, right) with
+// left = clamp(qi - 1), right = clamp(qi), bottom = clamp(qj - 1), top = clamp(qj).
+__global__ void env_quad_kernel(const float4* img, int w, int h, float4* q) {
+    const size_t n = (size_t)(w + 1) * (h + 1);
+    const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const int qj = (int)(r / (size_t)(w + 1)), qi = (int)(r - (size_t)qj * (w + 1));
+    const int l = qi > 0 ? qi - 1 : 0, rt = qi < w ? qi : w - 1;
+    const int bo = qj > 0 ? qj - 1 : 0, tp = qj < h ? qj : h - 1;
+    q[4 * r] = img[(size_t)bo * w + l];
+    q[4 * r + 1] = img[(size_t)bo * w + rt];
+    q[4 * r + 2] = img[(size_t)tp * w + l];
+    q[4 * r + 3] = img[(size_t)tp * w + rt];
+}
+
+static void free_env(pnrt_ctx* c) {
+    (void)hipFree(c->hdr); (void)hipFree(c->rnd); (void)hipFree(c->hdr_q); (void)hipFree(c->rnd_q);
+    c->hdr = c->rnd = c->hdr_q = c->rnd_q = nullptr;
+}
+
+static int env_quads(pnrt_ctx* c, int w, int h) {
+    const size_t n = (size_t)(w + 1) * (h + 1);
+    HIPCHK(c, hipMalloc(&c->hdr_q, n * 64));
+    HIPCHK(c, hipMalloc(&c->rnd_q, n * 64));
+    const unsigned g = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(env_quad_kernel, dim3(g), dim3(256), 0, c->stream, (const float4*)c->hdr, w, h, (float4*)c->hdr_q);
+    hipLaunchKernelGGL(env_quad_kernel, dim3(g), dim3(256), 0, c->stream, (const float4*)c->rnd, w, h, (float4*)c->rnd_q);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PNRT_OK;
+}
+
 int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int h) {
     if (!c) return PNRT_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, sync_all(c));
-    (void)hipFree(c->hdr); (void)hipFree(c->rnd);
-    c->hdr = c->rnd = nullptr;
+    free_env(c);
     c->scene.has_hdr = 0;
     if (!rgb) return PNRT_OK;
     if (!rnd || w <= 0 || h <= 0) return set_err(c, PNRT_E_ARG, "upload_env: bad arguments");
@@ -744,6 +780,7 @@ int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int 
     HIPCHK(c, hipMalloc(&c->rnd, b.size() * 16));
     HIPCHK(c, hipMemcpy(c->hdr, a.data(), a.size() * 16, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->rnd, b.data(), b.size() * 16, hipMemcpyHostToDevice));
+    if (int rc = env_quads(c, w, h)) return rc;
     c->scene.has_hdr = 1;
     c->scene.hdr_w = w; c->scene.hdr_h = h;
     return PNRT_OK;
@@ -754,8 +791,7 @@ int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
     if (!rgb || w <= 0 || h <= 0) return set_err(c, PNRT_E_ARG, "upload_env_build: bad arguments");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, sync_all(c));
-    (void)hipFree(c->hdr); (void)hipFree(c->rnd);
-    c->hdr = c->rnd = nullptr;
+    free_env(c);
     c->scene.has_hdr = 0;
     const size_t n = (size_t)w * h;
     std::vector<float4> a(n);
@@ -779,6 +815,7 @@ int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(tmp);
     if (e != hipSuccess) return set_err(c, PNRT_E_HIP, std::string("upload_env_build: ") + hipGetErrorString(e));
+    if (int rc = env_quads(c, w, h)) return rc;
     c->scene.has_hdr = 1;
     c->scene.hdr_w = w; c->scene.hdr_h = h;
     return PNRT_OK;
@@ -839,6 +876,8 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
     DevScene s = c->scene;
     s.hdr = static_cast<const float4*>(c->hdr);
     s.rnd = static_cast<const float4*>(c->rnd);
+    s.hdr_q = static_cast<const float4*>(c->hdr_q);
+    s.rnd_q = static_cast<const float4*>(c->rnd_q);
     s.n_tex = PT_MAX_TEXTURES;
     for (int i = 0; i < PT_MAX_TEXTURES; ++i) {
         s.tex[i] = static_cast<const uint32_t*>(c->tex[i]);

@@ -62,6 +62,11 @@ struct DevScene {
     int has_hdr, hdr_w, hdr_h;
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad
+    // the same two images as bilinear footprints: record (qj, qi), qi in [0, w],
+    // qj in [0, h], holds the 2x2 texels a lookup with left column qi - 1 and
+    // bottom row qj - 1 (clamped to the edge) reads -- one 64-B block per lookup
+    const float4* hdr_q;
+    const float4* rnd_q;
     int n_tex;
     const uint32_t* tex[PT_MAX_TEXTURES];   // RGBA8 texels
     int tex_w[PT_MAX_TEXTURES], tex_h[PT_MAX_TEXTURES];

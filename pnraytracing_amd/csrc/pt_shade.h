@@ -80,6 +80,26 @@ PN_DEV f3 taps_resolve(const Taps4& t) {
 PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
     return taps_resolve(taps_clamp(img, w, h, u, v));
 }
+// taps_clamp through the footprint records (DevScene::hdr_q / rnd_q): the same
+// four texels, bit for bit, from one 64-B record instead of two image rows.
+// Left column i0 and right column i1 = clamp(i0 + 1) select record qi = i0 + 1,
+// except at the left edge (i0 = i1 = 0: record 0, both columns 0).
+#ifndef PT_ENV_QUAD
+#define PT_ENV_QUAD 1
+#endif
+PN_DEV Taps4 taps_quad(const float4* img, const float4* quads, int w, int h, float u, float v) {
+    if (!PT_ENV_QUAD) return taps_clamp(img, w, h, u, v);
+    Taps4 t;
+    float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
+    float flu = floorf(fu), flv = floorf(fv);
+    t.a = fu - flu; t.b = fv - flv;
+    int i0 = wrap_clamp(flu, w), i1 = wrap_clamp(flu + 1.0f, w);
+    int j0 = wrap_clamp(flv, h), j1 = wrap_clamp(flv + 1.0f, h);
+    const int qi = (i1 == i0 && i0 == 0) ? 0 : i0 + 1, qj = (j1 == j0 && j0 == 0) ? 0 : j0 + 1;
+    const float4* r = quads + 4 * ((size_t)qj * (size_t)(w + 1) + (size_t)qi);
+    t.t00 = r[0]; t.t10 = r[1]; t.t01 = r[2]; t.t11 = r[3];
+    return t;
+}
 PN_DEV f3 texel_u8(const DevScene& s, uint32_t px) {
     return mk3(s.unorm8[px & 0xffu], s.unorm8[(px >> 8) & 0xffu], s.unorm8[(px >> 16) & 0xffu]);
 }
@@ -145,7 +165,7 @@ PN_DEV f3 env_color(const DevScene& s, f3 v) {
     u = u * 0.1591f; w = w * 0.3183f;
     u = u + 0.5f; w = w + 0.5f;
     w = 1.0f - w;
-    return sample_clamp(s.hdr, s.hdr_w, s.hdr_h, u, w);
+    return taps_resolve(taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, u, w));
 }
 
 // SampleHDRImage (:560-576) in two halves: env_dir turns the RandomHDR taps at
@@ -163,12 +183,12 @@ PN_DEV Taps4 env_dir(const DevScene& s, const Taps4& paramTaps, f3& L, float& pd
     float sinTheta = fmax_(1e-10f, st);
     float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
     pdf = pdf * convert;
-    return taps_clamp(s.hdr, s.hdr_w, s.hdr_h, param.x, param.y);
+    return taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, param.x, param.y);
 }
 
 // SampleHDRImage (:560-576); r1, r2 drawn by the caller in order
 PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
-    f3 param = WF_KO_ENV ? mk3(r1, r2, 0.5f) : sample_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
+    f3 param = WF_KO_ENV ? mk3(r1, r2, 0.5f) : taps_resolve(taps_quad(s.rnd, s.rnd_q, s.hdr_w, s.hdr_h, r1, r2));
     param.y = 1.0f - param.y;
     float phi = (2.0f * PT_PI) * (param.x - 0.5f);
     float theta = PT_PI * (param.y - 0.5f);
@@ -181,7 +201,7 @@ PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
     float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
     pdf = pdf * convert;
     if (WF_KO_ENV) return mk3(param.x, param.y, 0.5f);
-    return sample_clamp(s.hdr, s.hdr_w, s.hdr_h, param.x, param.y);
+    return taps_resolve(taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, param.x, param.y));
 }
 
 // ---- Disney BRDF (:649-849) -------------------------------------------------------

@@ -218,7 +218,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     const LightFetch lf = light_fetch(s, light_entry(s, uSel));
     Taps4 envTaps;
     if constexpr (EARLY >= 2) {
-        if (s.has_hdr) envTaps = taps_clamp(s.rnd, s.hdr_w, s.hdr_h, r1, r2);
+        if (s.has_hdr) envTaps = taps_quad(s.rnd, s.rnd_q, s.hdr_w, s.hdr_h, r1, r2);
     }
     Material m = get_material(s, hmat);
     asm volatile("" ::: "memory");
