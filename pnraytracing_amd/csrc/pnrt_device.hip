@@ -227,8 +227,11 @@ static WfLayout wf_layout(char* base, size_t n) {
     const size_t npad = (n + 255) / 256 * 256;
     size_t off = 0;
     for (PathSet& ps : L.set) {
-        float4** f4[] = {&ps.P0, &ps.P1, &ps.P2, &ps.P3, &ps.P4, &ps.P5, &ps.P6};
-        for (float4** q : f4) { *q = reinterpret_cast<float4*>(base + off); off += npad * 16; }
+        float4** f4[] = {&ps.P0, &ps.P1, &ps.P2, &ps.P3, &ps.P4, &ps.P5, &ps.P6, &ps.P7};
+        for (float4** q : f4) {
+            if (q == &ps.P7 && !WF_LIGHT_FROM_STATE) { *q = nullptr; continue; }
+            *q = reinterpret_cast<float4*>(base + off); off += npad * 16;
+        }
         ps.bcount = reinterpret_cast<uint32_t*>(base + off); off += (npad / 256) * 4;
         off = (off + 255) & ~(size_t)255;
     }
@@ -239,8 +242,8 @@ static WfLayout wf_layout(char* base, size_t n) {
     off = (off + 255) & ~(size_t)255;
     b.npad = (uint32_t)((n + 255) / 256 * 256);
     b.nseg_k = b.npad / 256;
-    // ray records of the queued kinds (light, env; + continuation without WF_CONT_FROM_STATE)
-    const size_t rec = (size_t)b.npad * 16 * (WF_CONT_FROM_STATE ? 2 : 3);
+    // ray records of the queued kinds (env; light / continuation unless traced from the state)
+    const size_t rec = (size_t)b.npad * 16 * WF_NQUEUED;
     b.rayO = reinterpret_cast<float4*>(base + off); off += rec;
     b.rayD = reinterpret_cast<float4*>(base + off); off += rec;
     b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;

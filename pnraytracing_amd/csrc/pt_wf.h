@@ -37,6 +37,17 @@
 #endif
 #define WF_TRACE_BLOCK 256
 #define WF_CHUNK 256u        // rays per dequeue
+#ifndef WF_CONT_FROM_STATE
+#define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued
+#endif
+#ifndef WF_LIGHT_FROM_STATE
+#define WF_LIGHT_FROM_STATE 1  // light shadow rays are traced from the path state (P0, P7), not queued
+#endif
+// ray kinds: 0 light shadow, 1 env shadow, 2 continuation; which have queued records,
+// and each queued kind's index among them (its npad-slot range in rayO / rayD)
+#define WF_QUEUED(k) (!((k) == 0 && WF_LIGHT_FROM_STATE) && !((k) == 2 && WF_CONT_FROM_STATE))
+#define WF_NQUEUED (WF_QUEUED(0) + WF_QUEUED(1) + WF_QUEUED(2))
+PN_DEV constexpr uint32_t wf_qidx(int k) { return (k > 0 && WF_QUEUED(0)) + (k > 1 && WF_QUEUED(1)); }
 
 // ray kinds a setup emitted (enqueue) ...
 #define WF_RLIGHT 2u
@@ -62,6 +73,7 @@ struct PathSet {
     float4* P4;   // LEnvironment.xyz, -    written iff the path has an env ray, read iff it is unoccluded
     float4* P5;   // Lo.xyz, bits(seed)
     float4* P6;   // throughput.xyz, bits(meta)
+    float4* P7;   // light shadow ray direction (WF_LIGHT_FROM_STATE; read by trace only)
     uint32_t* bcount;   // live paths of each setup block
 };
 
@@ -255,6 +267,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         f3 lightBRDF = disney(bc, lightL);
         LD = divs(muls(mul(lightBRDF, lf.li), pnm_fabs(dot(N, lightL))), pl);
         rays.dL = ldir;
+        if (WF_LIGHT_FROM_STATE) w.P7[i] = make_float4(ldir.x, ldir.y, ldir.z, 0.f);
         nfl |= WF_RLIGHT;
     }
     // stored as soon as final (shorter live ranges), and only when shade can use it:
@@ -341,21 +354,21 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
 #ifndef WF_SORT_OCTANT
 #define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
 #endif
-#ifndef WF_CONT_FROM_STATE
-#define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued
-#endif
 #define WF_NBIN 8
 PN_DEV int wf_dir_bin(const f3 d) {
     return WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
 }
 //
-// Continuation rays (WF_CONT_FROM_STATE): every live path has one and the setup
-// has just compacted the block's live paths to entries [256 j, 256 j + total),
-// so their segment IS that range of the path state -- origin P0.xyz, direction
-// P1.xyz, the same floats a ray record would copy.  Only the count is stored
-// (sorting them by octant measured neutral, 2 x 3 runs).
-PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays, uint32_t total) {
-    constexpr int NK = WF_CONT_FROM_STATE ? 2 : 3;     // kinds with queued ray records
+// Rays traced from the path state: every live path has a continuation ray, and a
+// light shadow ray whenever the scene has lights (the setup draws one for every
+// path, :878-909), and the setup has just compacted the block's live paths to
+// entries [256 j, 256 j + total) -- so the segment of such a kind IS that range
+// of the path state: origin P0.xyz (the offset origin both kinds start from),
+// direction P1.xyz (continuation) or P7.xyz (light), the same floats a ray
+// record would copy.  Only the count is stored.  (Sorting continuation rays by
+// octant measured neutral, 2 x 3 runs.)
+PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays, uint32_t total,
+                       bool lights) {
     // Inside a segment the rays are grouped by direction bin: rays with the same
     // signs take the same near/far choice at every node (:448), so a wave walks
     // the tree more coherently.  Slots within a bin come from LDS atomics (order
@@ -367,24 +380,29 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
     int oct[3];
     unsigned int rank[3];
 #pragma unroll
-    for (int k = 0; k < NK; ++k) {
+    for (int k = 0; k < 3; ++k) {
+        if (!WF_QUEUED(k)) continue;
         const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
         oct[k] = wf_dir_bin(d);
         rank[k] = (nfl & need[k]) ? atomicAdd(&bin[k][oct[k]], 1u) : 0u;
     }
     __syncthreads();
-    if (NK == 2 && threadIdx.x == 2) b.segcount[2 * b.nseg_k + blockIdx.x] = total;
-    if (threadIdx.x < NK) {                   // exclusive prefix over the bins of a kind
-        unsigned int run = 0;
-        for (int o = 0; o < WF_NBIN; ++o) { const unsigned int c = bin[threadIdx.x][o]; bin[threadIdx.x][o] = run; run += c; }
-        bin[threadIdx.x][WF_NBIN] = run;
-        b.segcount[threadIdx.x * b.nseg_k + blockIdx.x] = run;
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        if (WF_QUEUED(k)) {                   // exclusive prefix over the bins of a kind
+            unsigned int run = 0;
+            for (int o = 0; o < WF_NBIN; ++o) { const unsigned int c = bin[k][o]; bin[k][o] = run; run += c; }
+            bin[k][WF_NBIN] = run;
+            b.segcount[k * b.nseg_k + blockIdx.x] = run;
+        } else {
+            b.segcount[k * b.nseg_k + blockIdx.x] = (k == 2 || lights) ? total : 0u;
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < NK; ++k) {
-        if (nfl & need[k]) {
-            const size_t slot = (size_t)k * b.npad + (size_t)blockIdx.x * 256 + bin[k][oct[k]] + rank[k];
+    for (int k = 0; k < 3; ++k) {
+        if (WF_QUEUED(k) && (nfl & need[k])) {
+            const size_t slot = (size_t)wf_qidx(k) * b.npad + (size_t)blockIdx.x * 256 + bin[k][oct[k]] + rank[k];
             const f3 o = k == 1 ? rays.oP : rays.oOff;
             const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
             b.rayO[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(i));
@@ -440,7 +458,7 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
     BounceRays rays;
     if (cont) nfl = wf_setup_core<WF_GEN_EARLY>(s, fp, b, j, i, 0, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
-    wf_enqueue(b, j, nfl, rays, total);     // every lane of the wave reaches this point
+    wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
@@ -619,10 +637,15 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
                         uint32_t& p) {
-    // continuation rays: path entry = slot - 2 npad, read from the state the setup wrote
-    const bool fromState = WF_CONT_FROM_STATE && kind == 2;     // wave-uniform
-    const uint32_t e = fromState ? slot - 2u * b.npad : slot;
-    const float4 ro = (fromState ? b.wr.P0 : b.rayO)[e], rd = (fromState ? b.wr.P1 : b.rayD)[e];
+    // slot = kind * npad + position in the kind's range; kinds traced from the state
+    // the setup wrote read path entry e, queued kinds their record (see wf_enqueue)
+    const uint32_t e = slot - kind * b.npad;
+    const bool fromState = !WF_QUEUED(kind);     // wave-uniform
+    const uint32_t ri = (kind == 0 ? wf_qidx(0) : kind == 1 ? wf_qidx(1) : wf_qidx(2)) * b.npad + e;
+    const float4* O = fromState ? b.wr.P0 : b.rayO;
+    const float4* D = fromState ? (kind == 0 ? b.wr.P7 : b.wr.P1) : b.rayD;
+    const uint32_t at = fromState ? e : ri;
+    const float4 ro = O[at], rd = D[at];
     p = fromState ? e : __float_as_uint(ro.w);
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
@@ -884,5 +907,5 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     BounceRays rays;
     if (cont) nfl = wf_setup_core<WF_SHADE_EARLY>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
-    wf_enqueue(b, j, nfl, rays, total);     // every lane of the wave reaches this point
+    wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
 }
