@@ -203,7 +203,7 @@ static int upload(pnrt_ctx* c, const std::vector<T>& v, const T** out) {
 static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 
 #ifndef WF_TRACE_GRID_PCT
-#define WF_TRACE_GRID_PCT 40         // cap of the trace grid, % of full occupancy (three calls share the chip)
+#define WF_TRACE_GRID_PCT 50         // cap of the trace grid, % of full occupancy (three calls share the chip)
 #endif
 #ifndef WF_TRACE_PATHS_PER_BLOCK
 #define WF_TRACE_PATHS_PER_BLOCK 2048 // > 0: trace grid <= paths / this (small multi-GPU shares)
