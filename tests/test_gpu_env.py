@@ -60,3 +60,21 @@ def test_render_with_gpu_table(pt):
     pt.reset_accum()
     pt.render(0, 2)
     assert np.array_equal(pt.read_accum().view(np.uint32), a.view(np.uint32))
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (2, 3), (37, 13), (64, 1), (1, 50)])
+def test_render_odd_env_sizes_bitwise(pt, w, h):
+    """Environment lookups through the footprint records (edge clamps on every
+    side, one-texel rows and columns) equal the oracle's four-tap reads."""
+    import dataclasses
+    import pyoracle
+    rng = np.random.default_rng(7 * w + h)
+    rgb = (rng.random((h, w, 3)) ** 4 * 50).astype(np.float32)
+    c = dataclasses.replace(S.bunny_c2(64, 36), env_rgb=rgb, env_table=H.hdr_table(rgb))
+    pt.load(c)
+    pt.reset_accum()
+    pt.render(0, 2)
+    got = pt.read_accum()
+    ref, _ = pyoracle.Oracle(c).render(0, 2)
+    bad = np.argwhere(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=-1))
+    assert len(bad) == 0, f"{w}x{h} env: {len(bad)} pixels differ, first {bad[:3].tolist()}"
