@@ -206,7 +206,7 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #define WF_TRACE_GRID_PCT 50         // cap of the trace grid, % of full occupancy (three calls share the chip)
 #endif
 #ifndef WF_TRACE_PATHS_PER_BLOCK
-#define WF_TRACE_PATHS_PER_BLOCK 2048 // > 0: trace grid <= paths / this (small multi-GPU shares)
+#define WF_TRACE_PATHS_PER_BLOCK (8 * WF_TRACE_BLOCK) // > 0: trace grid <= paths / this (small multi-GPU shares)
 #endif
 
 // Wavefront buffers of one batch of n path slots, carved from `base`.

@@ -35,7 +35,11 @@
 #ifndef WF_QSTRIDE
 #define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
 #endif
-#define WF_TRACE_BLOCK 256
+#ifndef WF_TRACE_BLOCK
+#define WF_TRACE_BLOCK 256   // trace workgroup size (128 or 256)
+#endif
+#define WF_SPA_STRIDE (WF_TRACE_BLOCK * 8u)                 // LDS bytes per stack depth
+#define WF_SPA_SHIFT (WF_TRACE_BLOCK == 256 ? 11 : 10)
 #define WF_CHUNK 256u        // rays per dequeue
 #ifndef WF_CONT_FROM_STATE
 #define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued
@@ -478,29 +482,29 @@ PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& c
 
 // The lane's stack position is one register: spa = sp * 2048 + 8 * tl, the LDS
 // byte address of entry sp of lane tl (entries of one depth are 2048 B apart,
-// 256 lanes x 8 B), so sp = spa >> 11 and the lane's slot is spa & 2047 -- no
+// 256 lanes x 8 B; WF_SPA_STRIDE in general), so sp = spa >> 11 and the lane's slot is spa & 2047 -- no
 // separate per-lane base register (at 8 waves/SIMD the compiler spilled it).
 // Entries deeper than STK go to the global spill area, addressed from the same
 // value through one block-uniform buffer resource.
 PN_DEV uint32_t wf_ovf_off(const WfBufs& b, uint32_t spa, int stk) {
-    const uint32_t tl = (spa & 2047u) >> 3, k = (spa >> 11) - (uint32_t)stk;
+    const uint32_t tl = (spa & (WF_SPA_STRIDE - 1u)) >> 3, k = (spa >> WF_SPA_SHIFT) - (uint32_t)stk;
     return ((blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride + k) * 8u;
 }
 template <int STK>
 PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, uint32_t ref, float z) {
     const uint2 e = make_uint2(ref, __float_as_uint(z));
-    if (spa < STK * 2048u) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + spa) = e;
+    if (spa < STK * WF_SPA_STRIDE) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + spa) = e;
     else b.ovf[wf_ovf_off(b, spa, STK) / 8u] = e;
-    spa += 2048u;
+    spa += WF_SPA_STRIDE;
 }
 template <int STK>
 PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa) {
-    spa -= 2048u;
+    spa -= WF_SPA_STRIDE;
     // the common case is a ds_read; the rare spill read is a buffer load, which the
     // compiler cannot merge with the LDS read into one flat load (a flat load waits
     // for every outstanding vector-memory operation, stores included)
     uint2 e;
-    if (spa >= STK * 2048u) {
+    if (spa >= STK * WF_SPA_STRIDE) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)b.ovf, (short)0, 0x7fffffff, 0x00020000);
         const uint32_t off = wf_ovf_off(b, spa, STK);
@@ -619,8 +623,8 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     t.cur = isNode ? (goLeaf ? REF_NONE : go) : t.cur;
     // ---- next fetch target: pop when nothing is pending
     const bool idle = !done & (t.lc <= 0) & (t.cur == REF_NONE);
-    done = done | (idle & (t.spa < 2048u));
-    if (idle & (t.spa >= 2048u)) {
+    done = done | (idle & (t.spa < WF_SPA_STRIDE));
+    if (idle & (t.spa >= WF_SPA_STRIDE)) {
         const uint2 e = wf_pop<STK>(lds, b, t.spa);
         const float z = __uint_as_float(e.y);
         const bool culled = cull & (z > t.tMax * 1.000001f) & (z > 1e-20f);
@@ -751,7 +755,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
                     t.r = nr; t.tMax = ntmax; t.any = nany; rid = (kind << 30) | p;
-                    t.hitTri = -1; t.spa &= 2047u; t.cur = root; t.lt = nlt; t.lc = nlc;
+                    t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
                     busy = 1;
                 }
             }
