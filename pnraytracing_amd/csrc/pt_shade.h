@@ -84,6 +84,9 @@ PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
 // four texels, bit for bit, from one 64-B record instead of two image rows.
 // Left column i0 and right column i1 = clamp(i0 + 1) select record qi = i0 + 1,
 // except at the left edge (i0 = i1 = 0: record 0, both columns 0).
+#ifndef WF_KO_ENV
+#define WF_KO_ENV 0     // timing diagnostics (wrong images): 1 = environment lookups without their
+#endif                  // math or memory reads; 2 = the math, with every tap read from record 0
 #ifndef PT_ENV_QUAD
 #define PT_ENV_QUAD 1
 #endif
@@ -96,7 +99,7 @@ PN_DEV Taps4 taps_quad(const float4* img, const float4* quads, int w, int h, flo
     int i0 = wrap_clamp(flu, w), i1 = wrap_clamp(flu + 1.0f, w);
     int j0 = wrap_clamp(flv, h), j1 = wrap_clamp(flv + 1.0f, h);
     const int qi = (i1 == i0 && i0 == 0) ? 0 : i0 + 1, qj = (j1 == j0 && j0 == 0) ? 0 : j0 + 1;
-    const float4* r = quads + 4 * ((size_t)qj * (size_t)(w + 1) + (size_t)qi);
+    const float4* r = quads + (WF_KO_ENV == 2 ? 0 : 4 * ((size_t)qj * (size_t)(w + 1) + (size_t)qi));
     t.t00 = r[0]; t.t10 = r[1]; t.t01 = r[2]; t.t11 = r[3];
     return t;
 }
@@ -154,13 +157,10 @@ PN_DEV f3 sample_albedo(const DevScene& s, int t, float u, float v) {
                ((w00 * t00.z + w10 * t10.z) + w01 * t01.z) + w11 * t11.z);
 }
 
-#ifndef WF_KO_ENV
-#define WF_KO_ENV 0     // timing diagnostic: environment lookups without memory reads (wrong images)
-#endif
 // GetHDRImageColor (:181-193), invAtan = (0.1591, 0.3183) as written
 PN_DEV f3 env_color(const DevScene& s, f3 v) {
     if (!s.has_hdr) return mk3(0.f, 0.f, 0.f);
-    if (WF_KO_ENV) return mk3(v.x * 0.5f, 0.5f, 0.5f);
+    if (WF_KO_ENV == 1) return mk3(v.x * 0.5f, 0.5f, 0.5f);
     float u = pnm_atan2(v.z, v.x), w = pnm_asin(v.y);
     u = u * 0.1591f; w = w * 0.3183f;
     u = u + 0.5f; w = w + 0.5f;
@@ -188,7 +188,7 @@ PN_DEV Taps4 env_dir(const DevScene& s, const Taps4& paramTaps, f3& L, float& pd
 
 // SampleHDRImage (:560-576); r1, r2 drawn by the caller in order
 PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
-    f3 param = WF_KO_ENV ? mk3(r1, r2, 0.5f) : taps_resolve(taps_quad(s.rnd, s.rnd_q, s.hdr_w, s.hdr_h, r1, r2));
+    f3 param = WF_KO_ENV == 1 ? mk3(r1, r2, 0.5f) : taps_resolve(taps_quad(s.rnd, s.rnd_q, s.hdr_w, s.hdr_h, r1, r2));
     param.y = 1.0f - param.y;
     float phi = (2.0f * PT_PI) * (param.x - 0.5f);
     float theta = PT_PI * (param.y - 0.5f);
@@ -200,7 +200,7 @@ PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
     float sinTheta = fmax_(1e-10f, st);
     float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
     pdf = pdf * convert;
-    if (WF_KO_ENV) return mk3(param.x, param.y, 0.5f);
+    if (WF_KO_ENV == 1) return mk3(param.x, param.y, 0.5f);
     return taps_resolve(taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, param.x, param.y));
 }
 
