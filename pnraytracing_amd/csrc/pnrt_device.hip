@@ -82,7 +82,10 @@ struct pnrt_ctx {
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
     int kernel = 3;                        // 3 = wavefront (default), 1 = v1 one-lane-per-pixel
-    // Pipelined wavefront rendering.  pnrt_render call k uses pipe[k % WF_PIPES]: its own
+    // Pipelined wavefront rendering.  pnrt_render calls rotate over the pipes -- the
+    // first WF_PIPES_LARGE of them, or all WF_PIPES for small calls (a multi-GPU
+    // rank's share: its kernels are short, so a fourth call in flight fills the
+    // gaps of the other three's dependent chains; measured at N = 8).  A pipe is its own
     // worker stream(s) and primary / colour / path buffers, so call k+1 starts
     // while call k's kernels drain (one call's kernels fill the CUs the other's
     // trace kernel leaves idle while its last rays drain).  Only the blends are
@@ -102,6 +105,7 @@ struct pnrt_ctx {
     Pipe pipe[WF_PIPES];
     bool pipes_ready = false;
     uint64_t ncall = 0;
+    unsigned next_pipe = 0;
     int trace_grid = 0;
     int wf_stack_need = 0;                 // wide-traversal stack entries per lane (from upload)
     // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
@@ -342,7 +346,7 @@ static int pipes_init(pnrt_ctx* c) {
     return PNRT_OK;
 }
 
-// v3 wavefront, one pnrt_render call on pipe[ncall % 2]: primary pass, then per
+// v3 wavefront, one pnrt_render call on the next pipe: primary pass, then per
 // group of <= 8 frames two half-batches (each gen -> {trace -> shade} x depth) on
 // the pipe's two worker streams, then the frame-ordered blend on the blend stream.
 // The halves and consecutive calls are independent path sets, so running them
@@ -350,11 +354,14 @@ static int pipes_init(pnrt_ctx* c) {
 static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
     int rc;
     if ((rc = pipes_init(c))) return rc;
-    pnrt_ctx::Pipe& P = c->pipe[c->ncall % WF_PIPES];
     const size_t pix = (size_t)fp.rows * c->width;
     const uint32_t chunk = nf < WF_MAX_CHUNK_FRAMES ? nf : WF_MAX_CHUNK_FRAMES;
     const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
     const size_t per_frame = (size_t)tiles_x * tiles_y * 64;
+    const unsigned npipes = per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? WF_PIPES : WF_PIPES_LARGE;
+    const unsigned pi = c->next_pipe % npipes;
+    c->next_pipe = (pi + 1) % npipes;
+    pnrt_ctx::Pipe& P = c->pipe[pi];
     if (c->trace_grid == 0) {
         int per_cu = 0, cus = 0;
         HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false>, WF_TRACE_BLOCK, 0));
@@ -375,7 +382,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         return rc;
     ++c->ncall;
     hipStream_t w0 = P.w[0], w1 = P.w[1] ? P.w[1] : P.w[0];
-    // this pipe's buffers were last read by the blend of call ncall - WF_PIPES
+    // this pipe's buffers were last read by the blend of the call that used it last
     if (P.blend_pending) {
         HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
         if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));

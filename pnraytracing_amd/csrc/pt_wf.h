@@ -22,7 +22,13 @@
 #define WF_REFILL_PCT 40    // refill a wave when at most this % of its lanes still trace (tuned at 8 waves)
 #endif
 #ifndef WF_PIPES
-#define WF_PIPES 3          // pnrt_render calls in flight (buffer sets / worker streams; + the context stream = 4 HW queues)
+#define WF_PIPES 4          // buffer sets / worker streams: pnrt_render calls in flight at most
+#endif
+#ifndef WF_PIPES_LARGE
+#define WF_PIPES_LARGE (WF_PIPES > 3 ? 3 : WF_PIPES)   // calls in flight for large calls (+ the context
+#endif                                                // stream = the 4 HW queues of a process)
+#ifndef WF_SMALL_CALL_PATHS
+#define WF_SMALL_CALL_PATHS 1500000   // calls with fewer paths (multi-GPU shares) use all WF_PIPES sets
 #endif
 #ifndef WF_SPLIT
 #define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
