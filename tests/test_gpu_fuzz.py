@@ -7,6 +7,8 @@ light binary search) or none at all (GetLightIndex -> -1), environment on and
 off, RGB/RGBA/grey textures of odd widths on some meshes, odd image sizes and
 row-band shards, depth 1..4 -- the cases the fixed C1-C5 scenes do not reach.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -75,7 +77,8 @@ def pt():
         yield t
 
 
-@pytest.mark.parametrize("seed", list(range(24)))
+# PNRT_FUZZ_SEEDS=N widens the campaign (default 24 seeds; 400 were run once)
+@pytest.mark.parametrize("seed", list(range(int(os.environ.get("PNRT_FUZZ_SEEDS", "24")))))
 def test_random_scene_bitwise(pt, seed):
     from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL
     cfg, rng = random_scene(seed)
