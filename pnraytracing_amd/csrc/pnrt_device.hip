@@ -355,9 +355,13 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     int rc;
     if ((rc = pipes_init(c))) return rc;
     const size_t pix = (size_t)fp.rows * c->width;
-    const uint32_t chunk = nf < WF_MAX_CHUNK_FRAMES ? nf : WF_MAX_CHUNK_FRAMES;
     const int tiles_x = (c->width + 7) / 8, tiles_y = (fp.rows + 7) / 8;
     const size_t per_frame = (size_t)tiles_x * tiles_y * 64;
+    // frames per batch: at most WF_MAX_CHUNK_FRAMES, and few enough that every path
+    // slot fits the path state's slot field (large frames take fewer per batch)
+    if (per_frame > (size_t)WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: frame too large for one batch");
+    const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
+    const uint32_t chunk = nf < fit ? nf : fit;
     const unsigned npipes = per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? WF_PIPES : WF_PIPES_LARGE;
     const unsigned pi = c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;

@@ -188,6 +188,22 @@ def test_progressive_split_calls(pt):
     assert_bitwise(b, a, "render(0,1)+render(1,3) vs render(0,4)")
 
 
+def test_large_frame_batches(pt):
+    """An 8192x4320 frame holds more path slots than fit two frames in one batch
+    (2^26), so a full-frame call renders one frame per batch; a 1/16 row shard
+    of the same call fits all three frames in one batch.  Its rows must match."""
+    c = S.bunny_c2(8192, 4320)
+    pt.load(c)
+    pt.reset_accum()
+    pt.render(0, 3)
+    full = pt.read_accum()
+    pt.reset_accum()
+    pt.render(0, 3, 8, 16, 0)
+    part = pt.read_accum()
+    rows = (np.arange(c.height) // 8) % 16 == 0
+    assert_bitwise(part[rows], full[rows], "8192x4320: shard (one batch) vs full frame (one frame per batch)")
+
+
 def test_many_frames_and_calls(pt):
     """One call of 11 frames (two frame groups of <= 8 paths-per-pixel batches) and
     six calls in a row (the pipelined buffer sets rotate twice) both equal the
