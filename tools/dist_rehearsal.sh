@@ -1,12 +1,13 @@
 #!/bin/bash
-# Rehearse bench.py's multi-rank path on a 1-GPU box: 2 ranks share the GPU,
+# Rehearse bench.py's multi-rank path on a 1-GPU box: NPROC (default 2) ranks share the GPU,
 # gather staged through gloo; the gathered image must equal the 1-rank image.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 ARGS="--steps 2 --warmup 1 --no-cpu-baseline --config C2"
 timeout -k 10 300 python bench.py $ARGS --save-image gpurun_out/img_n1.npy > gpurun_out/dist_n1.log 2>&1 || exit $?
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29533 bench.py --gpus 2 --backend gloo $ARGS --save-image gpurun_out/img_n2.npy \
+NP=${NPROC:-2}
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP --master-addr 127.0.0.1 \
+    --master-port 29533 bench.py --gpus $NP --backend gloo $ARGS --save-image gpurun_out/img_n2.npy \
     > gpurun_out/dist_n2.log 2>&1 || exit $?
 python - <<'PY'
 import numpy as np, json
