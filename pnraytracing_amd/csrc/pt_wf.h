@@ -95,12 +95,14 @@ struct WfBufs {
     uint2* ovf;        // traversal stack spill, ovf_stride entries per trace lane
     uint32_t ovf_stride;
     unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
-    // ray queues, written by setup without atomics: setup block j compacts its
-    // paths' rays of kind k (light | env | continuation) into segment (k, j) =
-    // slots [k * npad + 256 j, +segcount[k * nseg_k + j]) as ready-to-trace
-    // records: rayO = (origin, bits(path slot)), rayD = (direction, -)
-    float4* rayO;            // [3 * npad]  (.w = path entry j)
-    float4* rayD;            // [3 * npad]
+    // ray queues, written by setup without atomics: segment (k, j) of kind k
+    // (light | env | continuation) and setup block j = trace slots
+    // [k * npad + 256 j, +segcount[k * nseg_k + j]).  Queued kinds (WF_QUEUED:
+    // env) store ready-to-trace records there -- rayO = (origin, bits(path
+    // entry)), rayD = (direction, -), at wf_qidx(k) * npad + the slot's offset;
+    // the other kinds are read from the path state (see wf_enqueue)
+    float4* rayO;            // [WF_NQUEUED * npad]  (.w = path entry j)
+    float4* rayD;            // [WF_NQUEUED * npad]
     unsigned int* segcount;  // [3 * nseg_k]
     uint32_t npad;           // n rounded up to 256
     uint32_t nseg_k;         // setup blocks = segments per kind
