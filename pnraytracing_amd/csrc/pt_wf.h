@@ -557,8 +557,8 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
 #endif
 #define WF_NSUB (256 / WF_SUB)
-#ifndef WF_CONT_FIRST
-#define WF_CONT_FIRST 1     // dequeue continuation-ray segments before the shadow-ray segments
+#ifndef WF_KIND_ORDER
+#define WF_KIND_ORDER 0x210 // sweep order of the ray kinds, one hex digit each (0 light, 1 env, 2 continuation)
 #endif
 #ifndef WF_TIMING
 #define WF_TIMING 0         // diagnostic builds: per-wave timestamps of the trace kernel
@@ -731,13 +731,14 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
                 else {
                     // one dequeue = WF_SUB rays of a segment (finer grains balance the
-                    // drain at the end of the launch).  Kind order of the sweep:
-                    // continuation rays (closest hit, the longest traversals) first, so
-                    // the launch ends on short shadow rays
+                    // drain at the end of the launch).  Kind order of the sweep
+                    // (WF_KIND_ORDER): continuation rays (closest hit, the longest
+                    // traversals) first, then env shadow rays, so the launch ends
+                    // on the short light shadow rays
                     const uint32_t sj = seg / WF_NSUB, part = seg - sj * WF_NSUB;
                     const uint32_t qk = sj / b.nseg_k;
                     const uint32_t j = sj - qk * b.nseg_k;
-                    ckind = WF_CONT_FIRST ? (qk == 0u ? 2u : qk - 1u) : qk;
+                    ckind = (uint32_t)(WF_KIND_ORDER >> (4 * (2 - (int)qk))) & 0xfu;
                     const uint32_t cnt = b.segcount[ckind * b.nseg_k + j];
                     const uint32_t lo = min(part * (uint32_t)WF_SUB, cnt);
                     next = ckind * b.npad + j * 256u + lo;
