@@ -18,6 +18,7 @@
 #include "pn_oracle.h"
 #include "pn_libm.h"
 #include <stdlib.h>
+#include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -48,6 +49,9 @@ static inline v3 cross(v3 a, v3 b) {
 static inline float length(v3 a) { return sqrtf(dot(a, a)); }
 /* normalize(x) = x / length(x) (GLSL 4.50 8.5) */
 static inline v3 normalize(v3 a) { return divs(a, length(a)); }
+/* glm::normalize (glm 0.9.9.8 func_geometric.inl:88, inversesqrt = 1/sqrt):
+ * only for the CPU-header semantics of pno_intersect */
+static v3 glm_normalize(v3 a) { return muls(a, 1.0f / sqrtf(dot(a, a))); }
 /* min/max: GLSL undefined for NaN; here NaN-dropping (IEEE minNum/maxNum),
  * first operand on ties. */
 static inline float fmin_(float a, float b) { return (b < a || a != a) ? b : a; }
@@ -85,7 +89,17 @@ typedef struct {
     uint32_t seed;
     int bounce;
     pno_stats* st;
+    /* 0: the GLSL's rules (what pno_render uses).  Otherwise a mask of the
+     * reference CPU headers' rules, for pinning against them (pno_intersect):
+     * SEM_TIE   triangle.hpp:75-76 rejects tScaled >= tMax*det (ties keep the
+     *           FIRST triangle; the GLSL keeps the last),
+     * SEM_BOX   bound.hpp:31-47 clips the slab to [0, tMax] with std::max/min,
+     * SEM_NORM  glm::normalize = v * (1/sqrt(dot(v,v))) (glm func_geometric.inl:88). */
+    int sem;
 } Ctx;
+#define SEM_TIE 1
+#define SEM_BOX 2
+#define SEM_NORM 4
 
 /* texelFetch on an RGB32F buffer texture: out-of-range -> 0 (robust access). */
 static inline v3 texel(const float* buf, int n_texels, int i) {
@@ -280,6 +294,28 @@ static int BoundIntersect(Bound b, Ray r) {
     return t1 >= t0;
 }
 
+/* bound.hpp:31-47 BoundIntersect of the reference's CPU headers: slab clipped
+ * to [0, tMax], std::swap / std::max / std::min (NaN operands drop out of
+ * max/min because `a < b` is false).  Only for pno_intersect's pinning mode. */
+static int BoundIntersectCPU(Bound b, Ray r, float* h0, float* h1) {
+    float t0 = 0.0f, t1 = r.tMax;
+    for (int i = 0; i < 3; ++i) {
+        float invDir = 1.0f / comp(r.dir, i);
+        float tNear = (comp(b.pMin, i) - comp(r.origin, i)) * invDir;
+        float tFar = (comp(b.pMax, i) - comp(r.origin, i)) * invDir;
+        if (tNear > tFar) { float t = tNear; tNear = tFar; tFar = t; }
+        t0 = (t0 < tNear) ? tNear : t0;       /* std::max(t0, tNear) */
+        t1 = (tFar < t1) ? tFar : t1;         /* std::min(t1, tFar)  */
+        if (t0 > t1) return 0;
+    }
+    if (h0) *h0 = t0;
+    if (h1) *h1 = t1;
+    return 1;
+}
+static int box_hit(const Ctx* c, Bound b, const Ray* r) {
+    return (c->sem & SEM_BOX) ? BoundIntersectCPU(b, *r, 0, 0) : BoundIntersect(b, *r);
+}
+
 /* ---- GetLightIndex (:237-251) ------------------------------------------- */
 static int GetLightIndex(Ctx* c, float u) {
     int lightsSize = c->s->n_lights;
@@ -300,7 +336,7 @@ static inline void swapf(float* a, float* b) { float t = *a; *a = *b; *b = t; }
  * :360-424): PBRT-v3 watertight test, NOT Moller-Trumbore.  Returns 1 and
  * e0,e1,e2,det,tScaled when accepted against ray.tMax with the GLSL's `>`
  * (equal t is ACCEPTED, so ties go to the later triangle). */
-static int tri_test(v3 p0, v3 p1, v3 p2, const Ray* ray,
+static int tri_test(v3 p0, v3 p1, v3 p2, const Ray* ray, int sem,
                     float* e0o, float* e1o, float* e2o, float* deto, float* tso) {
     v3 P0 = sub(p0, ray->origin), P1 = sub(p1, ray->origin), P2 = sub(p2, ray->origin);
     v3 rd = ray->dir;
@@ -322,8 +358,13 @@ static int tri_test(v3 p0, v3 p1, v3 p2, const Ray* ray,
     float det = (e0 + e1) + e2;
     if (det == 0) return 0;
     float tScaled = (e0 * P0.z + e1 * P1.z) + e2 * P2.z;
-    if (det > 0 && (tScaled <= 0 || tScaled > ray->tMax * det)) return 0;
-    if (det < 0 && (tScaled >= 0 || tScaled < ray->tMax * det)) return 0;
+    if (!(sem & SEM_TIE)) {
+        if (det > 0 && (tScaled <= 0 || tScaled > ray->tMax * det)) return 0;
+        if (det < 0 && (tScaled >= 0 || tScaled < ray->tMax * det)) return 0;
+    } else {                                  /* triangle.hpp:75-76 */
+        if (det > 0 && (tScaled <= 0 || tScaled >= ray->tMax * det)) return 0;
+        if (det < 0 && (tScaled >= 0 || tScaled <= ray->tMax * det)) return 0;
+    }
     *e0o = e0; *e1o = e1; *e2o = e2; *deto = det; *tso = tScaled;
     return 1;
 }
@@ -337,7 +378,7 @@ static int TriangleIntersect(Ctx* c, Triangle tri, Ray* ray, Interaction* isect)
     v3 p0 = v0.position, p1 = v1.position, p2 = v2.position;
     float e0, e1, e2, det, tScaled;
     c->st->tri_tests++;
-    if (!tri_test(p0, p1, p2, ray, &e0, &e1, &e2, &det, &tScaled)) return 0;
+    if (!tri_test(p0, p1, p2, ray, c->sem, &e0, &e1, &e2, &det, &tScaled)) return 0;
     c->st->tri_hits++;
     float invDet = 1.0f / det;
     float t = tScaled * invDet;
@@ -346,12 +387,13 @@ static int TriangleIntersect(Ctx* c, Triangle tri, Ray* ray, Interaction* isect)
     uvHit.x = (v0.texcoord.x * b0 + v1.texcoord.x * b1) + v2.texcoord.x * b2;
     uvHit.y = (v0.texcoord.y * b0 + v1.texcoord.y * b1) + v2.texcoord.y * b2;
     v3 nHit;
+    v3 (*nrm)(v3) = (c->sem & SEM_NORM) ? glm_normalize : normalize;
     if (iszero3(v0.normal) || iszero3(v1.normal) || iszero3(v2.normal))
-        nHit = normalize(cross(sub(p1, p0), sub(p2, p0)));
+        nHit = nrm(cross(sub(p1, p0), sub(p2, p0)));
     else
         nHit = add(add(muls(v0.normal, b0), muls(v1.normal, b1)), muls(v2.normal, b2));
     if (dot(nHit, ray->dir) > 0) nHit = neg(nHit);
-    nHit = normalize(nHit);
+    nHit = nrm(nHit);
     isect->position = add(add(smul(b0, p0), smul(b1, p1)), smul(b2, p2));
     isect->normal = nHit;
     isect->texcoord = uvHit;
@@ -369,7 +411,7 @@ static int TriangleIntersectP(Ctx* c, Triangle tri, const Ray* ray) {
     v3 p2 = GetVertexPosition(c, tri.indices[2]);
     float e0, e1, e2, det, tScaled;
     c->st->tri_tests++;
-    return tri_test(p0, p1, p2, ray, &e0, &e1, &e2, &det, &tScaled);
+    return tri_test(p0, p1, p2, ray, c->sem, &e0, &e1, &e2, &det, &tScaled);
 }
 
 /* BVHIntersect (:429-461) / BVHIntersectP (:464-494).  128-entry stack; the
@@ -384,7 +426,7 @@ static int BVHIntersect(Ctx* c, Ray* r, Interaction* isect) {
         int curId = nodeStack[--top];
         BVHNode node = GetBVHNode(c, curId);
         c->st->node_pops++;
-        if (!BoundIntersect(node.bound, *r)) continue;
+        if (!box_hit(c, node.bound, r)) continue;
         if (node.rightChild == -1) {
             for (int i = node.startIndex; i < node.endIndex; ++i)
                 if (TriangleIntersect(c, GetTriangle(c, i), r, isect)) hit = 1;
@@ -394,11 +436,11 @@ static int BVHIntersect(Ctx* c, Ray* r, Interaction* isect) {
             if (comp(r->dir, node.axis) < 0) {
                 nodeStack[top++] = curId + 1;
                 BVHNode rc = GetBVHNode(c, node.rightChild);
-                if (BoundIntersect(rc.bound, *r)) nodeStack[top++] = node.rightChild;
+                if (box_hit(c, rc.bound, r)) nodeStack[top++] = node.rightChild;
             } else {
                 nodeStack[top++] = node.rightChild;
                 BVHNode lc = GetBVHNode(c, curId + 1);
-                if (BoundIntersect(lc.bound, *r)) nodeStack[top++] = curId + 1;
+                if (box_hit(c, lc.bound, r)) nodeStack[top++] = curId + 1;
             }
         }
     }
@@ -413,7 +455,7 @@ static int BVHIntersectP(Ctx* c, const Ray* r) {
         int curId = nodeStack[--top];
         BVHNode node = GetBVHNode(c, curId);
         c->st->node_pops++;
-        if (!BoundIntersect(node.bound, *r)) continue;
+        if (!box_hit(c, node.bound, r)) continue;
         if (node.rightChild == -1) {
             for (int i = node.startIndex; i < node.endIndex; ++i)
                 if (TriangleIntersectP(c, GetTriangle(c, i), r)) return 1;
@@ -423,15 +465,75 @@ static int BVHIntersectP(Ctx* c, const Ray* r) {
             if (comp(r->dir, node.axis) < 0) {
                 nodeStack[top++] = curId + 1;
                 BVHNode rc = GetBVHNode(c, node.rightChild);
-                if (BoundIntersect(rc.bound, *r)) nodeStack[top++] = node.rightChild;
+                if (box_hit(c, rc.bound, r)) nodeStack[top++] = node.rightChild;
             } else {
                 nodeStack[top++] = node.rightChild;
                 BVHNode lc = GetBVHNode(c, curId + 1);
-                if (BoundIntersect(lc.bound, *r)) nodeStack[top++] = curId + 1;
+                if (box_hit(c, lc.bound, r)) nodeStack[top++] = curId + 1;
             }
         }
     }
     return 0;
+}
+
+/* ---- pinning hook: the intersection routines on caller rays ------------- */
+static inline uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static void put_isect(uint32_t* o, int hit, const Interaction* is, float tmax_after) {
+    memset(o, 0, 13 * sizeof(uint32_t));
+    o[0] = (uint32_t)hit;
+    if (hit && is) {
+        o[1] = fbits(is->position.x); o[2] = fbits(is->position.y); o[3] = fbits(is->position.z);
+        o[4] = fbits(is->normal.x); o[5] = fbits(is->normal.y); o[6] = fbits(is->normal.z);
+        o[7] = fbits(is->texcoord.x); o[8] = fbits(is->texcoord.y);
+        o[9] = (uint32_t)is->textureId; o[10] = (uint32_t)is->materialId; o[11] = fbits(is->time);
+    }
+    o[12] = fbits(tmax_after);
+}
+
+int pno_intersect(const pno_scene* scene, const float* rays, int n, int kind, int sem,
+                  const int* idx, uint32_t* out, int threads) {
+    if (!scene || !rays || !out || n < 0 || kind < 0 || kind > 4) return -1;
+    if ((kind >= 2) && !idx) return -1;
+#ifdef _OPENMP
+    int nt = threads > 0 ? threads : omp_get_max_threads();
+#else
+    int nt = 1; (void)threads;
+#endif
+    int overflow = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 256) num_threads(nt) reduction(|:overflow)
+#endif
+    for (int i = 0; i < n; ++i) {
+        pno_stats st;
+        memset(&st, 0, sizeof st);
+        Ctx c;
+        memset(&c, 0, sizeof c);
+        c.s = scene; c.st = &st; c.sem = sem;
+        const float* q = rays + 7 * (size_t)i;
+        Ray r;
+        r.origin = V3(q[0], q[1], q[2]); r.dir = V3(q[3], q[4], q[5]); r.tMax = q[6];
+        Interaction is;
+        memset(&is, 0, sizeof is);
+        uint32_t* o = out + 13 * (size_t)i;
+        int hit = 0;
+        switch (kind) {
+        case 0: hit = BVHIntersect(&c, &r, &is); put_isect(o, hit, &is, r.tMax); break;
+        case 1: hit = BVHIntersectP(&c, &r); put_isect(o, hit, 0, r.tMax); break;
+        case 2: hit = TriangleIntersect(&c, GetTriangle(&c, idx[i]), &r, &is); put_isect(o, hit, &is, r.tMax); break;
+        case 3: hit = TriangleIntersectP(&c, GetTriangle(&c, idx[i]), &r); put_isect(o, hit, 0, r.tMax); break;
+        default: {
+            Bound b = GetBVHNode(&c, idx[i]).bound;
+            float h0 = 0.0f, h1 = 0.0f;
+            const int cpu = (sem & SEM_BOX) != 0;
+            hit = cpu ? BoundIntersectCPU(b, r, &h0, &h1) : BoundIntersect(b, r);
+            memset(o, 0, 13 * sizeof(uint32_t));
+            o[0] = (uint32_t)hit;
+            if (hit && cpu) { o[1] = fbits(h0); o[2] = fbits(h1); }
+        }
+        }
+        overflow |= st.stack_overflow;
+    }
+    return overflow ? -6 : 0;
 }
 
 /* ---- RNG (:499-557) ------------------------------------------------------- */
@@ -807,7 +909,7 @@ int pno_render(const pno_scene* scene, const pno_frame* frame,
         int tid = 0;
 #endif
         Ctx c;
-        c.s = scene; c.f = frame; c.st = &per[tid]; c.py = y_begin + ri * y_step;
+        c.s = scene; c.f = frame; c.st = &per[tid]; c.py = y_begin + ri * y_step; c.sem = 0;
         for (int x = 0; x < frame->width; ++x) {
             c.px = x;
             float* p = accum + 4 * ((size_t)c.py * frame->width + x);

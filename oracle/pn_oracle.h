@@ -7,11 +7,18 @@
  * Pinning status (see DESIGN.md "Oracle"):
  *   - RNG (wang_hash), Sobol, camera, host arrays: pinned by known answers
  *     computed from the reference's own sources (SURVEY 8c KATs, oracle/_ref).
- *   - The integrator's image output: PARITY UNPINNED by the reference itself
- *     (the GLSL cannot execute in this container -- no GL 4.5 context / no
- *     glslang -- and the reference ships no golden images or tests).  Its
- *     faithfulness rests on line-by-line restatement of ray_tracing.comp,
- *     with every function citing the lines it follows.
+ *   - Ray/triangle, slab and BVH traversal arithmetic: PINNED bit for bit to
+ *     the reference's own CPU code (triangle.hpp, bound.hpp, BVH.hpp compiled
+ *     here, oracle/ref/isect_driver.cpp) on ~3.4M seeded ray queries per
+ *     scene over C1/C2/C4/C5, with the three documented rule differences
+ *     (ties, slab clipping, glm::normalize) switched by pno_intersect's `sem`
+ *     (tests/test_isect_pin.py).
+ *   - The shading half (Disney BRDF, sampling, MIS, env lookups): unpinned by
+ *     the reference itself (the GLSL cannot execute in this container -- no
+ *     GL 4.5 context / no glslang -- and the reference has no CPU version of
+ *     it and no golden images or tests).  Its faithfulness rests on
+ *     line-by-line restatement of ray_tracing.comp, with every function
+ *     citing the lines it follows.
  *
  * Inputs are the reference's own flattened float arrays exactly as main.cpp
  * packs them (main.cpp:409-524): vertex 15 f, material 18 f, triangle 6 f,
@@ -78,6 +85,22 @@ int pno_render(const pno_scene* scene, const pno_frame* frame,
  * fn: 0 sin, 1 cos, 2 atan2(a,b), 3 asin, 4 log, 5 pow(a,b), 6 exp2,
  *     7 sqrt, 8 a/b, 9 float(uint32 bits of a), 10 wang_hash(bits of a) */
 void pno_math_eval(int fn, const float* a, const float* b, float* out, int n);
+
+/* Pinning hook (tests only): the oracle's intersection routines on caller
+ * rays, n x 7 floats (origin, dir, tMax).  kind 0: closest hit over the BVH
+ * (BVHIntersect, :429-461), 1: any hit (BVHIntersectP, :464-494), 2: one
+ * triangle idx[i] (TriangleIntersect, :254-357), 3: TriangleIntersectP
+ * (:360-427), 4: the box of node idx[i] (BoundIntersect, :213-228).
+ * sem 0: the GLSL's rules (as rendered); otherwise a mask of the reference
+ * CPU headers' rules: 1 triangle.hpp:75-76 `>=` ties, 2 bound.hpp:31-47
+ * [0,tMax] slab clipping with std::max/min, 4 glm::normalize; sem 7 makes the
+ * shared arithmetic comparable bit for bit with the reference compiled here
+ * (oracle/ref/isect_driver.cpp).
+ * out: n x 13 words: hit, position[3], normal[3], texcoord[2], textureId,
+ * materialId, time (floats as bits; zeros when no hit), ray tMax after; for
+ * kind 4 with sem & 2: hit, t0, t1.  Returns 0, -1 bad args, -6 stack overflow. */
+int pno_intersect(const pno_scene* scene, const float* rays, int n, int kind, int sem,
+                  const int* idx, uint32_t* out, int threads);
 
 /* Known-answer helpers. */
 uint32_t pno_wang_hash(uint32_t* seed);

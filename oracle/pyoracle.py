@@ -93,6 +93,9 @@ def lib():
         L.pno_math_eval.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.pno_wang_hash.restype = ctypes.c_uint32
         L.pno_wang_hash.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+        L.pno_intersect.restype = ctypes.c_int
+        L.pno_intersect.argtypes = [ctypes.POINTER(Scene), ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.pno_sobol.restype = ctypes.c_float
         L.pno_sobol.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         _lib = L
@@ -163,6 +166,26 @@ class Oracle:
         if rc != 0:
             raise RuntimeError(f"pno_render failed ({rc})")
         return accum, st.as_dict()
+
+    def intersect(self, rays: np.ndarray, kind: int, sem: int, idx: np.ndarray | None = None,
+                  threads: int = 0) -> np.ndarray:
+        """The oracle's intersection routines on caller rays (pn_oracle.h
+        pno_intersect): rays (n, 7) float32 = origin, dir, tMax; kind 0 closest
+        hit, 1 any hit, 2/3 triangle idx[i], 4 box of node idx[i]; sem 0 = the
+        GLSL's rules, 1 = the reference CPU headers' rules.  Returns (n, 13) u32."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 7)
+        n = len(rays)
+        out = np.zeros((n, 13), np.uint32)
+        ip = None
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, np.int32)
+            assert len(idx) == n
+            ip = idx.ctypes.data
+        rc = lib().pno_intersect(ctypes.byref(self.scene), rays.ctypes.data, n, kind, sem, ip, out.ctypes.data,
+                                 threads)
+        if rc != 0:
+            raise RuntimeError(f"pno_intersect failed ({rc})")
+        return out
 
 
 def math_eval(fn: int, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:

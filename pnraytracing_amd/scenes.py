@@ -120,7 +120,7 @@ def checker_texture(w: int, h: int, ch: int = 3, seed: int = 7):
     return (px.reshape(-1), w, h, ch)
 
 
-def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144, bvh_tracer=None) -> SceneConfig:
+def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144, env=True, bvh_tracer=None) -> SceneConfig:
     """C3: CornellBox() with its commented-out "marry" model (main.cpp:209) -- a
     UV-mapped ~50k-triangle figure stand-in textured with MC003_Kozakura_Mari.png
     (RGBA 2048x1024, texture unit 5) -- plus SceneFlat()'s metal boards
@@ -138,7 +138,7 @@ def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144, bvh_tracer=None) ->
         bm = H.Material(baseColor=(0.83, 0.83, 0.83), metallic=met, roughness=rough)
         sb.add_model(board, [H.translate(-1.6 + 1.6 * k, 0.6, z), H.rotate(50.0 - 15.0 * k, 1, 0, 0),
                              H.scale(0.012, 1.0, 0.004)], bm, f"board{k + 1}", texture_ids=[1])
-    rgb, tab = _env_1k()
+    rgb, tab = _env_1k() if env else (None, None)
     tex = [load_texture(MARI_PNG), checker_texture(333, 97, 3)]
     return SceneConfig("C3-marry", sb.build(bvh_tracer), _cornell_camera(width, height), width, height, spp,
                        env_rgb=rgb, env_table=tab, textures=tex,
@@ -146,7 +146,7 @@ def marry_c3(width=1920, height=1080, spp=4, nu=176, nv=144, bvh_tracer=None) ->
                                    f"+ metal boards (RGB 333x97) + 1k env")
 
 
-def teapot_c4(width=1920, height=1080, spp=4, bvh_tracer=None) -> SceneConfig:
+def teapot_c4(width=1920, height=1080, spp=4, env=True, bvh_tracer=None) -> SceneConfig:
     """C4: teapot() scene (main.cpp:329-347) + an emissive quad and the 1k env,
     so the light, environment and BSDF pdfs are all active."""
     sb = H.SceneBuilder()
@@ -157,21 +157,24 @@ def teapot_c4(width=1920, height=1080, spp=4, bvh_tracer=None) -> SceneConfig:
     light = H.Material(baseColor=(0.73, 0.73, 0.73), emssive=(8.0, 8.0, 8.0))
     sb.add_model(H.mesh_quad(27.5), [H.translate(1.5, 3.0, 1.0), H.rotate(180.0, 0, 0, 1), H.scale(0.02)],
                  light, "area_light")
-    rgb, tab = _env_1k()
+    rgb, tab = _env_1k() if env else (None, None)
     cam = H.camera_update((0, 5, 5), (0, 0, 0), (0, 1, 0), 45.0, np.float32(width) / np.float32(height))
     return SceneConfig("C4-teapot", sb.build(bvh_tracer), cam, width, height, spp, env_rgb=rgb, env_table=tab,
                        description="teapot stand-in + floor + area light + 1k env")
 
 
-def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, env_h=2048, bvh_tracer=None) -> SceneConfig:
+def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, env_h=2048, env=True,
+                 bvh_tracer=None) -> SceneConfig:
     """C5: 4,194,304-triangle displaced sphere in the Cornell box, 4k synthetic env."""
     sb = H.SceneBuilder()
     m = H.Material(baseColor=(0.65, 0.65, 0.65))
     big = H.mesh_displaced_sphere(nu, nv, BUNNY_RADIUS, BUNNY_CENTER, 0.12, 0x5EED)
     sb.add_model(big, [H.translate(0, 0, -2), H.scale(8)], m, "sphere4m")
     _cornell_walls(sb, m)
-    rgb = H.synthetic_hdr(env_w, env_h, 0x5EED)
-    tab = H.hdr_table(rgb)
+    rgb = tab = None
+    if env:
+        rgb = H.synthetic_hdr(env_w, env_h, 0x5EED)
+        tab = H.hdr_table(rgb)
     return SceneConfig("C5-synthetic4m", sb.build(bvh_tracer), _cornell_camera(width, height), width, height, spp,
                        env_rgb=rgb, env_table=tab,
                        description=f"{nu * nv * 2}-tri displaced sphere + {env_w}x{env_h} synthetic env")

@@ -117,6 +117,16 @@ def build_recorded(fn, **kw):
     return cfg, rec_holder["r"]
 
 
+ASPECT_1080 = float(np.float32(1920) / np.float32(1080))
+ASPECT_2160 = float(np.float32(3840) / np.float32(2160))
+CORNELL_CAM = ((0, 2.8, 7), (0, 2.8, 0), (0, 1, 0), 45.0)
+# (fixture key, scenes.* builder, camera args as main.cpp passes them, builder kwargs)
+SCENES = [("C2", S.bunny_c2, CORNELL_CAM + (ASPECT_1080,), {"env": False}),
+          ("C3", S.marry_c3, CORNELL_CAM + (ASPECT_1080,), {"env": False}),
+          ("C4", S.teapot_c4, ((0, 5, 5), (0, 0, 0), (0, 1, 0), 45.0, ASPECT_1080), {"env": False}),
+          ("C5", S.synthetic_c5, CORNELL_CAM + (ASPECT_2160,), {"env": False})]
+
+
 def main():
     if not os.path.exists(DRIVER):
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle", "ref"), f"REF={REF}"], check=True)
@@ -130,11 +140,9 @@ def main():
                         materials=np.stack(rec1.mats))
     print("C1:", {k: v.shape for k, v in ref1.items()})
 
-    # ---- C2 / C4: hashes + samples of the reference-built arrays ------------------------------
-    for key, fn, cam in [("C2", S.bunny_c2, ((0, 2.8, 7), (0, 2.8, 0), (0, 1, 0), 45.0, float(np.float32(1920) / np.float32(1080)))),
-                         ("C4", S.teapot_c4, ((0, 5, 5), (0, 0, 0), (0, 1, 0), 45.0, float(np.float32(1920) / np.float32(1080))))]:
-        kw = {"env": False} if key == "C2" else {}
-        cfg, rec = build_recorded(fn, **kw) if key == "C2" else build_recorded(fn)
+    # ---- C2-C5: hashes + samples of the reference-built arrays ------------------------------
+    for key, fn, cam, kw in SCENES:
+        cfg, rec = build_recorded(fn, **kw)
         ref = run_driver(driver_input(rec, cam))
         rng = np.random.default_rng(7)
         samp = {k: sorted(rng.choice(len(ref[k]), min(64, len(ref[k])), replace=False).tolist())

@@ -54,10 +54,15 @@ def test_c1_model_matrices_match_glm():
         np.testing.assert_array_equal(bits(H.model_matrix(o)), bits(ref["matrices"][i]))
 
 
-@pytest.mark.parametrize("key", ["C2", "C4"])
+BUILDERS = {"C2": S.bunny_c2, "C3": S.marry_c3, "C4": S.teapot_c4, "C5": S.synthetic_c5}
+
+
+@pytest.mark.parametrize("key", ["C2", "C3", "C4", "C5"])
 def test_scene_arrays_hash_equal_reference_build(key):
+    """Whole arrays (sha256) and 64 sampled rows of each: C5 is the 4.19M-triangle
+    build (4,228,165 nodes) of SURVEY 8c item 1."""
     fx = FIX[key]
-    cfg = S.bunny_c2(env=False) if key == "C2" else S.teapot_c4()
+    cfg = BUILDERS[key](env=False)
     p = cfg.packed
     for k in ("vertices", "triangles", "nodes", "lights"):
         arr = getattr(p, k)
