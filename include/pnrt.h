@@ -51,6 +51,7 @@ typedef struct {
 #define PNRT_KERNEL_V1 0x100    /* A/B baseline: one lane per pixel, frames in-lane        */
                                 /* default: wavefront (setup / trace / shade per bounce)   */
 
+/* "pnrt-mi355x <version> (gfx950) src <sha256[:16] of the device sources>" */
 const char* pnrt_version(void);
 
 /* Replaces WindowInit's GL context (main.cpp:64-94): bind HIP device. */

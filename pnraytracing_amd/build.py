@@ -11,6 +11,7 @@ same IEEE binary32 operation sequences (bit-exact parity).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -50,6 +51,16 @@ def build_host(force=False):
     return out
 
 
+def device_source_hash() -> str:
+    """sha256 (16 hex) of the device library's sources, stamped into
+    pnrt_version() so a stale prebuilt libpnrt.so is detectable."""
+    h = hashlib.sha256()
+    for d in [os.path.join(CSRC, d) for d in DEVICE_DEPS] + [os.path.join(INC, "pnrt.h")]:
+        h.update(os.path.basename(d).encode())
+        h.update(open(d, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def build_device(force=False, extra=()):
     out = os.path.join(PKG, "libpnrt.so")
     deps = [os.path.join(CSRC, d) for d in DEVICE_DEPS] + [os.path.join(INC, "pnrt.h")]
@@ -58,9 +69,25 @@ def build_device(force=False, extra=()):
                "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-rdc",
                # no SLP packing into v_pk_*_f32: the register pairs it needs cost the
                # trace kernel a wave per SIMD and the setup kernels one
-               "-fno-slp-vectorize", "-I", INC,
+               "-fno-slp-vectorize", f'-DPNRT_SRC_HASH="{device_source_hash()}"', "-I", INC,
                *extra, *[os.path.join(CSRC, s) for s in DEVICE_SRCS], "-o", out]
         _run(cmd)
+    return out
+
+
+def build_abi_caller(force=False):
+    """tests/abi/c_abi_render: a compiled C++ caller of include/pnrt.h +
+    include/pnrt_host.h linked against the two libraries (TEST-ONLY; exercises
+    the drop-in boundary without Python, tests/test_gpu_c_abi.py)."""
+    src = os.path.join(REPO, "tests", "abi", "c_abi_render.cpp")
+    out = os.path.join(REPO, "tests", "abi", "c_abi_render")
+    deps = [src, os.path.join(INC, "pnrt.h"), os.path.join(INC, "pnrt_host.h"),
+            os.path.join(PKG, "libpnrt.so"), os.path.join(PKG, "libpnrt_host.so")]
+    if not os.path.exists(src) or not all(os.path.exists(d) for d in deps):
+        return None
+    if force or _stale(out, deps):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-I", INC, src, "-o", out, "-L", PKG, "-lpnrt", "-lpnrt_host",
+              "-Wl,-rpath,$ORIGIN/../../pnraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib"])
     return out
 
 
@@ -75,6 +102,7 @@ def build_oracle(force=False):
 def build_all(force=False):
     build_host(force)
     build_device(force)
+    build_abi_caller(force)
     build_oracle(force)
 
 

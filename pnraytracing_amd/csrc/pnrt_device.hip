@@ -90,8 +90,11 @@ struct pnrt_ctx {
     // while call k's kernels drain (one call's kernels fill the CUs the other's
     // trace kernel leaves idle while its last rays drain).  Only the blends are
     // ordered: they run in call order on the context stream, which therefore
-    // sees each call's finished image.  (Worker streams + the context stream
-    // stay within the 4 hardware queues a process gets: GPU_MAX_HW_QUEUES.)
+    // sees each call's finished image.  The fourth pipe (small calls only) is
+    // created only when the process has more than 4 hardware queues
+    // (GPU_MAX_HW_QUEUES, HIP's default 4): with 4, its worker would share the
+    // context stream's queue and serialise behind the blends, so small calls
+    // rotate over the first three like large ones (n_pipes_small).
     struct Pipe {
         hipStream_t w[2] = {nullptr, nullptr};
         hipEvent_t ev_prim = nullptr, ev_join[2] = {nullptr, nullptr}, ev_blend = nullptr;
@@ -103,6 +106,8 @@ struct pnrt_ctx {
         bool blend_pending = false;  // ev_blend guards the colour buffer's last reader
     };
     Pipe pipe[WF_PIPES];
+    unsigned n_pipes_small = WF_PIPES;     // pipes small calls rotate over (pipes_init)
+    hipEvent_t ev_switch = nullptr;        // orders a pnrt_set_stream switch after the old stream's work
     bool pipes_ready = false;
     uint64_t ncall = 0;
     unsigned next_pipe = 0;
@@ -337,7 +342,11 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
 static int pipes_init(pnrt_ctx* c) {
     if (c->pipes_ready) return PNRT_OK;
     c->pipes_ready = true;
-    for (auto& P : c->pipe) {
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    const int hw_queues = (q && atoi(q) > 0) ? atoi(q) : 4;
+    c->n_pipes_small = hw_queues > 4 ? WF_PIPES : WF_PIPES_LARGE;
+    for (unsigned i = 0; i < c->n_pipes_small; ++i) {
+        auto& P = c->pipe[i];
         for (int k = 0; k < (WF_SPLIT ? 2 : 1); ++k) HIPCHK(c, hipStreamCreateWithFlags(&P.w[k], hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&P.ev_prim, hipEventDisableTiming));
         for (auto& e : P.ev_join) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -362,7 +371,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     if (per_frame > (size_t)WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: frame too large for one batch");
     const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
     const uint32_t chunk = nf < fit ? nf : fit;
-    const unsigned npipes = per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? WF_PIPES : WF_PIPES_LARGE;
+    const unsigned npipes = per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small : WF_PIPES_LARGE;
     const unsigned pi = c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;
     pnrt_ctx::Pipe& P = c->pipe[pi];
@@ -444,7 +453,12 @@ static void free_env(pnrt_ctx* c);
 
 extern "C" {
 
-const char* pnrt_version(void) { return "pnrt-mi355x 0.1 (gfx950)"; }
+#ifndef PNRT_SRC_HASH
+#define PNRT_SRC_HASH "unknown"
+#endif
+// the build stamps the sha256 of the device sources (pnraytracing_amd/build.py),
+// so a stale prebuilt library shipped beside newer sources is detectable
+const char* pnrt_version(void) { return "pnrt-mi355x 0.2 (gfx950) src " PNRT_SRC_HASH; }
 
 int pnrt_create(int device, pnrt_ctx** out) {
     if (!out) return PNRT_E_ARG;
@@ -503,6 +517,7 @@ void pnrt_destroy(pnrt_ctx* c) {
 
     for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -513,7 +528,16 @@ void* pnrt_get_stream(pnrt_ctx* c) { return c ? static_cast<void*>(c->own_stream
 
 int pnrt_set_stream(pnrt_ctx* c, void* s) {
     if (!c) return PNRT_E_ARG;
-    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    if (ns == c->stream) return PNRT_OK;
+    // blends (frame-ordered read-modify-writes of accum), pack_rows and
+    // read_accum run on c->stream: the new stream starts after everything the
+    // old one holds, so no blend of a later call overtakes a pending one
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->ev_switch) HIPCHK(c, hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_switch, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(ns, c->ev_switch, 0));
+    c->stream = ns;
     return PNRT_OK;
 }
 
@@ -736,6 +760,7 @@ int pnrt_upload_texture(pnrt_ctx* c, int slot, const uint8_t* px, int w, int h, 
             }
             texels[(size_t)j * w + i] = rgb[0] | (rgb[1] << 8) | (rgb[2] << 16);
         }
+    HIPCHK(c, sync_all(c));             // pipelined calls may still sample the old texture
     (void)hipFree(c->tex[slot]);
     c->tex[slot] = nullptr;
     HIPCHK(c, hipMalloc(&c->tex[slot], texels.size() * 4));

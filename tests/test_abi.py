@@ -27,8 +27,14 @@ def test_library_exports_declared_symbols(header, path):
 
 
 def test_device_library_typed_and_versioned():
+    """pnrt_version() carries the sha256 of the device sources it was built from
+    (build.py stamps it): a stale prebuilt libpnrt.so beside newer sources --
+    e.g. one shipped to the GPU box -- fails here instead of testing old code."""
+    from pnraytracing_amd import build
     lib = N.device_lib()
-    assert b"gfx950" in lib.pnrt_version()
+    v = lib.pnrt_version().decode()
+    assert "gfx950" in v
+    assert v.endswith("src " + build.device_source_hash()), (v, build.device_source_hash())
 
 
 def test_device_create_fails_loudly_without_gpu():

@@ -91,3 +91,14 @@ def test_oracle_c1_stats_sane():
     assert st["samples"] == 32 * 32 and st["stack_overflow"] == 0
     assert np.isfinite(acc).all() and (acc[..., :3] >= 0).all() and (acc[..., :3] <= 1).all()
     assert (acc[..., 3] == 1).all()
+
+
+def test_c1_image_fixture_is_current_oracle():
+    """tests/golden/c1_oracle_image.npz (the C-ABI caller's expected image) is the
+    current oracle's render, bit for bit."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_c1_image
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_oracle_image.npz"))
+    np.testing.assert_array_equal(make_c1_image.render().view(np.uint32), gold["image"].view(np.uint32))
