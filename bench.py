@@ -15,15 +15,34 @@ N > 1: one process per GPU; the image rows are dealt in 8-row bands
 accumulated rows are gathered to rank 0 over RCCL every step (strong
 scaling: the frame is fixed, its rows are split).
 
-Prints ONE JSON line (rank 0) with roofline and cpu_baseline objects; see
-DESIGN.md "Measurement" for every field's derivation.
+Prints ONE JSON line (rank 0).  Roofline of the dominant kernel (pt_wf_trace),
+every figure measured by this run:
+  traffic   fabric bytes per trace launch, 2 x FETCH_SIZE + WRITE_SIZE from two
+            rocprofv3 --pmc passes that this script runs as child processes
+            BEFORE it touches the GPU (N = 1; MI355X_MICROARCH.md: gfx950
+            FETCH_SIZE counts half the bytes);
+  kernel_ms the trace launch's EXCLUSIVE duration: HIP events around every
+            trace launch during extra steps rendered with PNRT_SERIAL (one call
+            in flight, full-occupancy grid), after the timed region;
+  achieved  traffic / kernel_ms, against the 8 TB/s HBM peak (frac).
+The kernel's own request stream (device-layout fetches from the census of a
+WF_STATS build, profiles/census.json, used only when its source hash matches
+the loaded library) is reported beside it against the L2 bandwidth, and the
+SURVEY 8d reference-literal byte count as reference_bytes (never divided by a
+peak).  The timed steps themselves run the default pipelined renderer.
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import platform
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -33,6 +52,11 @@ sys.path.insert(0, REPO)
 
 BAND = 8
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 (8 XCDs) ~34.5 TB/s
+# rocprofv3 --pmc passes (one run each; TCC block: FETCH_SIZE uses 3 counters, WRITE_SIZE 2)
+PMC_PASSES = [("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum")]
+KSHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
+          "pt_primary_kernel": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
 
 
 def parse():
@@ -45,25 +69,134 @@ def parse():
     ap.add_argument("--kernel", default="v3", choices=["v1", "v3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes")
+    ap.add_argument("--pmc-timeout", type=int, default=240, help="seconds per PMC pass (killed after)")
+    ap.add_argument("--serial-steps", type=int, default=2,
+                    help="extra PNRT_SERIAL steps after the timed region for exclusive kernel times (0: skip)")
+    ap.add_argument("--serial", action="store_true",
+                    help="time the steps themselves with PNRT_SERIAL (one call in flight): for the rocprofv3 "
+                         "--stats run whose trace-kernel average is the roofline's exclusive kernel_ms")
     ap.add_argument("--save-image", default="")
     ap.add_argument("--spp", type=int, default=0, help="experiment: samples per step other than the config's 4")
     ap.add_argument("--kernel-times", action="store_true",
-                    help="time every kernel class with HIP events (default: only the dominant kernel)")
+                    help="time every kernel class with HIP events in the timed region (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
+    ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)   # a PMC pass's workload: no output
     return ap.parse_args()
 
 
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+# ---- host facts ------------------------------------------------------------------------------
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+# ---- live PMC (child processes, before this process initialises the GPU) --------------------
+def _read_counters(d):
+    """{kernel class: {counter: average per dispatch}, "_dispatches": {class: n}}"""
+    per = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "").strip()
+            if k not in KSHORT:
+                continue
+            key = (KSHORT[k], r["Dispatch_Id"])
+            per.setdefault(key, {})
+            per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    acc, nd = {}, {}
+    for (k, _), cs in per.items():
+        nd[k] = nd.get(k, 0) + 1
+        for c, v in cs.items():
+            acc.setdefault(k, {}).setdefault(c, []).append(v)
+    out = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+    out["_dispatches"] = nd
+    return out
+
+
+def live_pmc(args):
+    """Two rocprofv3 --kernel-trace --pmc passes over a short run of this same
+    workload (child processes: this process has not touched the GPU yet).
+    Returns {class: {"bytes_per_launch", "launches_per_step", "l2_hit_rate"}}
+    or None when rocprofv3 is absent or a pass fails."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        log("rocprofv3 not found: no live PMC")
+        return None
+    tmp = tempfile.mkdtemp(prefix="pnrt_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    steps, warm = 2, 1
+    counters = {}
+    try:
+        for i, group in enumerate(PMC_PASSES):
+            d = os.path.join(tmp, f"p{i}")
+            cmd = ["timeout", "-s", "KILL", str(args.pmc_timeout), exe, "--kernel-trace", "--pmc", *group,
+                   "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--child", "--config", args.config, "--mode", args.mode,
+                   "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
+            if args.spp:
+                cmd += ["--spp", str(args.spp)]
+            log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
+            t = time.perf_counter()
+            with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
+                r = subprocess.run(cmd, stdout=lf, stderr=subprocess.STDOUT, env=env)
+            if r.returncode != 0:
+                log(f"PMC pass {i + 1} failed (rc {r.returncode}); see {tmp}/p{i}.log")
+                return None
+            log(f"PMC pass {i + 1} done in {time.perf_counter() - t:.1f}s")
+            got = _read_counters(d)
+            nd = got.pop("_dispatches")
+            for k, cs in got.items():
+                counters.setdefault(k, {}).update(cs)
+                counters[k]["_n"] = nd.get(k, 0)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    res = {}
+    for k, cs in counters.items():
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        e = {"bytes_per_launch": (2.0 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0,
+             "launches_per_step": cs["_n"] / (steps + warm)}
+        if "TCC_HIT_sum" in cs:
+            e["l2_hit_rate"] = cs["TCC_HIT_sum"] / max(cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"], 1.0)
+        res[k] = e
+    return res or None
+
+
+def stored_keyed(path, key, src_hash):
+    """An entry of a profiles/*.json file, only if recorded for these sources."""
+    path = os.path.join(REPO, "profiles", path)
+    if not os.path.exists(path):
+        return None
+    e = json.load(open(path)).get(key)
+    if not e or e.get("source_hash") != src_hash:
+        return None
+    return e
+
+
+# ---- CPU baseline ------------------------------------------------------------------------------
 def cpu_baseline(cfg, target_s: float):
-    """CPU oracle (the C restatement of ray_tracing.comp, OpenMP over rows) on a
-    bounded row sample of the same workload; returns (dict, bytes_per_sample)."""
+    """CPU oracle (the C restatement of ray_tracing.comp, OpenMP over rows) on
+    whole 1080p 4-spp iterations of the same workload until ~target_s, plus C1
+    (the reference's CPU-runnable config) at full size; returns (dict, counters)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
+    from pnraytracing_amd import scenes
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 64))
     o = pyoracle.Oracle(cfg)
     H = cfg.height
-    # whole-frame 4-spp iterations of the same workload until ~target_s (max 8)
     acc = np.zeros((H, cfg.width, 4), np.float32)
     tot = None
     it = 0
@@ -76,34 +209,42 @@ def cpu_baseline(cfg, target_s: float):
             break
     dt = time.perf_counter() - t
     n = tot["samples"]
-    bps = {"bytes_per_sample": pyoracle.algorithmic_bytes(tot) / n,
-           "trace_bytes_per_sample": pyoracle.bounce_traversal_bytes(tot) / n}
-    return ({"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-             "sample": f"{cfg.name}: {it} full {cfg.width}x{H} iterations x {cfg.spp} spp = {n} samples "
-                       f"in {dt:.1f}s, oracle/pn_oracle.c OpenMP {threads} threads"},
-            bps, tot)
-
-
-def stored(path, cfg_name):
-    path = os.path.join(REPO, "profiles", path)
-    if not os.path.exists(path):
-        return None
-    return json.load(open(path)).get(cfg_name)
+    # C1: Cornell box, 256x256, 1 spp per frame, depth 4 (BASELINE configs[0]); frames until ~1 s
+    c1 = scenes.cornell_c1()
+    o1 = pyoracle.Oracle(c1)
+    a1 = np.zeros((c1.height, c1.width, 4), np.float32)
+    f1, t1 = 0, time.perf_counter()
+    while f1 < 64 and (f1 < 4 or time.perf_counter() - t1 < 1.0):
+        o1.render(f1, 1, accum=a1, threads=threads)
+        f1 += 1
+    d1 = time.perf_counter() - t1
+    cpu = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": f"{cfg.name}: {it} full {cfg.width}x{H} iterations x {cfg.spp} spp = {n} samples "
+                     f"in {dt:.1f}s, oracle/pn_oracle.c OpenMP {threads} threads",
+           "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+           "c1": {"value": round(f1 * c1.width * c1.height / d1 / 1e6, 4), "unit": "Msamples/s",
+                  "sample": f"C1 256x256 x {f1} frames (1 spp each, depth 4) in {d1:.2f}s"}}
+    return cpu, tot
 
 
 def main():
     args = parse()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # live PMC first, while this process has not initialised the GPU (the passes are
+    # child processes under rocprofv3)
+    pmc = None
+    if world == 1 and not args.child and not args.no_pmc:
+        pmc = live_pmc(args)
+    if world > 1:
         # multi-rank: RCCL adds a stream of its own beside the library's four (own +
         # three workers); 8 hardware queues keep it off theirs (set before HIP starts)
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
+    if world != args.gpus and rank == 0 and not args.child:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     ndev = torch.cuda.device_count()
     if ndev and local >= ndev:          # rehearsal of N ranks on fewer GPUs (gloo only)
@@ -117,26 +258,33 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from pnraytracing_amd import scenes
+    from pnraytracing_amd import build, host, scenes
     from pnraytracing_amd.dist import ShardedFrame
-    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer
+    from pnraytracing_amd.tracer import KERNEL_V1, SERIAL, TRAVERSE_EXACT, TRAVERSE_ZCULL, PathTracer
 
     builders = {"C2": scenes.bunny_c2, "C3": scenes.marry_c3, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
+    t = time.perf_counter()
     cfg = builders[args.config]()
+    scene_s = time.perf_counter() - t
     if args.spp:
         cfg.spp = args.spp
     W, H, spp = cfg.width, cfg.height, cfg.spp
 
     pt = PathTracer(local)
     # torch works on the library's own stream (created with the context, before its
-    # three worker streams): a fifth stream of torch's own would share one of the
+    # worker streams): a further stream of torch's own would share one of the
     # process's 4 hardware queues with a busy stream (measured -4 %)
     stream = torch.cuda.ExternalStream(pt.stream_handle())
     torch.cuda.set_stream(stream)
     pt.set_stream(stream.cuda_stream)
     opts = (TRAVERSE_ZCULL if args.mode == "zcull" else TRAVERSE_EXACT) | {"v1": KERNEL_V1, "v3": 0}[args.kernel]
+    if args.serial:
+        opts |= SERIAL
+    t = time.perf_counter()
     pt.load(cfg, opts)
+    upload_s = time.perf_counter() - t
     info = pt.device_info()
+    version = pt.version()
 
     sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
     image = None
@@ -155,11 +303,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.child:                             # a PMC pass: the profiler sees the launches; done
+        for k in range(args.steps):
+            step(args.warmup + k)
+        torch.cuda.synchronize()
+        pt.close()
+        return
     # live per-kernel timing: the library brackets every launch with HIP events
-    # recorded on the stream it launches on (pnrt_profile_enable)
-    # only the dominant kernel is bracketed unless --kernel-times: every event record
-    # is a queue packet between launches of the overlapped calls
-    pt.profile_select(None if args.kernel_times else [{"v1": "v1", "v3": "trace"}[args.kernel]])
+    # recorded on the stream it launches on (pnrt_profile_enable); only the dominant
+    # kernel is bracketed unless --kernel-times (every event record is a queue packet
+    # between launches of the overlapped calls)
+    kname = {"v1": "v1", "v3": "trace"}[args.kernel]
+    pt.profile_select(None if args.kernel_times else [kname])
     pt.profile_enable(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -173,47 +328,102 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = pt.profile_read()
     pt.profile_enable(False)
-    kname = {"v1": "v1", "v3": "trace"}[args.kernel]
     k_ms_total, k_launches = prof[kname]
-    kern_ms = k_ms_total / max(k_launches, 1)                  # average launch duration
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda" if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    kern_ms_pipe = k_ms_total / max(k_launches, 1)             # average launch duration, pipelined
+    launches_per_step = k_launches / args.steps
 
     if args.save_image and rank == 0:
         img = (image.cpu().numpy() if world > 1 else pt.read_accum())
         np.save(args.save_image, img)
 
+    # exclusive kernel times: PNRT_SERIAL steps (one call in flight, full trace grid)
+    excl = {}
+    if args.serial_steps > 0:
+        pt.set_options(opts | SERIAL)
+        pt.profile_select(None)
+        pt.profile_enable(True)
+        for k in range(args.serial_steps):
+            sf.render(spp * (args.warmup + args.steps + k), spp)
+        torch.cuda.synchronize()
+        ser = pt.profile_read()
+        pt.profile_enable(False)
+        pt.set_options(opts)
+        excl = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / args.serial_steps}
+                for k, (ms, n) in ser.items() if n}
+    kern_ms = excl[kname]["ms_per_launch"] if kname in excl else None
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms_pipe, kern_ms or 0.0], dtype=torch.float64,
+                         device="cuda" if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_pipe, kern_ms = float(t[0]), float(t[1]), (float(t[2]) or None)
+
     samples = W * H * spp * args.steps
     value = samples / elapsed / 1e6
-    line = None
     if rank == 0:
+        # one-shot setup, reported beside the step rate: host scene build
+        # (ModelOutput + BuildBVH + packing), the BuildBVH part alone on the host and on
+        # the GPU (pnrt_bvh_build, incl. PCIe; same arrays), and the upload (pnrt_*)
+        setup = {"scene_build_s": round(scene_s, 3), "bvh_build_host_s": round(cfg.packed.bvh_seconds, 4),
+                 "upload_s": round(upload_s, 3)}
+        if cfg.packed.tri_bounds is not None:
+            tb = cfg.packed.tri_bounds
+            pt.build_bvh(tb[: min(len(tb), 4096)])                    # module / allocation warm-up
+            t = time.perf_counter()
+            nodes, _, _ = pt.build_bvh(tb)
+            setup["bvh_build_gpu_s"] = round(time.perf_counter() - t, 4)
+            setup["bvh_gpu_identical"] = bool(np.array_equal(nodes.view(np.uint32), cfg.packed.nodes.view(np.uint32)))
+
         cpu = None
-        bps = None
+        counts = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu, bps, _ = cpu_baseline(cfg, args.cpu_seconds)
-        if bps is None:
-            bps = stored("algorithmic_bytes.json", cfg.name)
+            cpu, counts = cpu_baseline(cfg, args.cpu_seconds)
         rows0 = sf.my_rows
         samples_per_step = rows0 * W * spp
-        launches_per_step = k_launches / args.steps
-        achieved = path = None
-        if bps:
-            # dominant kernel: algorithmic bytes of one launch / its average duration
-            per_sample = bps["trace_bytes_per_sample"] if args.kernel == "v3" else bps["bytes_per_sample"]
-            bytes_per_launch = per_sample * samples_per_step / launches_per_step
-            achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-            # SURVEY 8d whole-path figure: all algorithmic bytes / wall time per step
-            path_gbs = bps["bytes_per_sample"] * samples_per_step * args.steps / elapsed / 1e9
-            path = {"bytes_per_sample": round(bps["bytes_per_sample"], 1), "achieved": round(path_gbs, 2),
-                    "frac": round(path_gbs / HBM_PEAK_GBS, 4)}
-        traffic = None
-        pmc = stored("pmc.json", f"{cfg.name}/{kname}")
-        if pmc and pmc.get("hbm_bytes_per_launch"):
-            traffic = round(pmc["hbm_bytes_per_launch"] * rows0 / pmc.get("rows", H))
+        src_hash = build.device_source_hash()
+        ref_bytes = None
+        if counts:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import pyoracle
+            per = (pyoracle.bounce_traversal_bytes(counts) if args.kernel == "v3"
+                   else pyoracle.algorithmic_bytes(counts)) / counts["samples"]
+            ref_bytes = round(per * samples_per_step / launches_per_step)
+
+        traffic = l2hit = None
+        traffic_src = None
+        step_traffic = None
+        if pmc and kname in pmc:
+            traffic, l2hit = pmc[kname]["bytes_per_launch"], pmc[kname].get("l2_hit_rate")
+            traffic_src = "live rocprofv3 --pmc (FETCH_SIZE; WRITE_SIZE + TCC_HIT/MISS), 2 x FETCH_SIZE + WRITE_SIZE"
+            step_traffic = {k: {"bytes_per_launch": round(e["bytes_per_launch"]),
+                                "launches_per_step": round(e["launches_per_step"], 3),
+                                "l2_hit_rate": round(e["l2_hit_rate"], 4) if "l2_hit_rate" in e else None}
+                            for k, e in pmc.items()}
+            step_traffic["total_bytes_per_step"] = round(sum(e["bytes_per_launch"] * e["launches_per_step"]
+                                                             for e in pmc.values()))
+        elif world == 1:
+            e = stored_keyed("pmc.json", f"{cfg.name}/{kname}", src_hash)
+            if e and e.get("hbm_bytes_per_launch"):
+                traffic, l2hit = e["hbm_bytes_per_launch"], e.get("l2_hit_rate")
+                traffic_src = "profiles/pmc.json (recorded for these sources)"
+        if traffic is not None and world > 1:
+            traffic = None                     # PMC is per-process at N = 1 only
+        achieved = traffic / (kern_ms * 1e-3) / 1e9 if (traffic and kern_ms) else None
+        census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
+        requested = None
+        if census and kern_ms:
+            rb = census["requested_bytes_per_launch"] * rows0 / census.get("rows", H)
+            requested = {"bytes_per_launch": round(rb), "achieved": round(rb / (kern_ms * 1e-3) / 1e9, 1),
+                         "peak": L2_PEAK_GBS, "unit": "GB/s",
+                         "frac_of_l2": round(rb / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
+                         "source": "profiles/census.json (WF_STATS build of these sources)"}
+        checks = None
+        if kern_ms:
+            checks = {"launches_x_kernel_ms": round(launches_per_step * kern_ms, 4),
+                      "le_ms_per_step": launches_per_step * kern_ms <= elapsed / args.steps * 1e3,
+                      "frac_le_1": (achieved / HBM_PEAK_GBS <= 1.0) if achieved else None}
         kernels = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / args.steps}
                    for k, (ms, n) in prof.items() if n}
+        kfull = {"v1": "pt_render_kernel", "v3": "pt_wf_trace"}[args.kernel]
         line = {
             "metric": "Msamples/sec (whole node) at 1920x1080, 4spp/iter; fraction of HBM roofline",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -223,19 +433,25 @@ def main():
             "config": {"workload": f"{cfg.name}: {cfg.description}", "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
-                       "kernel": {"v1": "pt_render_kernel", "v3": "pt_wf_trace"}[args.kernel]},
+                       "kernel": kfull},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic,
-                         "kernel": {"v1": "pt_render_kernel", "v3": "pt_wf_trace"}[args.kernel],
-                         "kernel_ms": round(kern_ms, 4),
-                         "algorithmic_bytes_per_launch": round(bytes_per_launch) if bps else None,
-                         "path": path},
+                         "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
+                         "l2_hit_rate": round(l2hit, 4) if l2hit is not None else None,
+                         "kernel": kfull, "kernel_ms": kern_ms, "kernel_ms_timing": "exclusive (PNRT_SERIAL steps)",
+                         "kernel_ms_pipelined": round(kern_ms_pipe, 4), "launches_per_step": launches_per_step,
+                         "checks": checks,
+                         "limiter": "dependent-fetch latency (L1-hit chains), not HBM: DESIGN.md section 4",
+                         "requested": requested,
+                         "reference_bytes_per_launch": ref_bytes},
             "kernels": kernels,
+            "kernels_exclusive": excl or None,
+            "fabric_traffic": step_traffic,
+            "setup": setup,
             "cpu_baseline": cpu,
             "device": {"bvh_interior_nodes": info["n_interior"], "max_depth": info["max_depth"],
-                       "scene_bytes": info["device_bytes"]},
+                       "scene_bytes": info["device_bytes"], "library": version},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

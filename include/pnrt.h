@@ -49,6 +49,9 @@ typedef struct {
 #define PNRT_TRAVERSE_EXACT 0   /* the reference's box visits (no tMax culling)      */
 #define PNRT_TRAVERSE_ZCULL 1   /* + provably result-neutral z-slab culling (default) */
 #define PNRT_KERNEL_V1 0x100    /* A/B baseline: one lane per pixel, frames in-lane        */
+#define PNRT_SERIAL 0x200       /* measurement: one pnrt_render call in flight and a full- */
+                                /* occupancy trace grid, so a kernel's launch duration is  */
+                                /* its exclusive time (same images; slower end to end)     */
                                 /* default: wavefront (setup / trace / shade per bounce)   */
 
 /* "pnrt-mi355x <version> (gfx950) src <sha256[:16] of the device sources>" */

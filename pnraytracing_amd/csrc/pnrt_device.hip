@@ -82,6 +82,7 @@ struct pnrt_ctx {
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
     int kernel = 3;                        // 3 = wavefront (default), 1 = v1 one-lane-per-pixel
+    bool serial = false;                   // PNRT_SERIAL: one call in flight, full trace grid (measurement)
     // Pipelined wavefront rendering.  pnrt_render calls rotate over the pipes -- the
     // first WF_PIPES_LARGE of them, or all WF_PIPES for small calls (a multi-GPU
     // rank's share: its kernels are short, so a fourth call in flight fills the
@@ -267,7 +268,7 @@ static WfLayout wf_layout(char* base, size_t n) {
 // multi-GPU frame) take a proportional part of the chip, and no launch more than
 // WF_TRACE_GRID_PCT %, so the calls in flight trace side by side instead of queueing.
 static unsigned trace_grid_for(const pnrt_ctx* c, size_t n) {
-    const size_t gmax = (size_t)c->trace_grid * WF_TRACE_GRID_PCT / 100;
+    const size_t gmax = (size_t)c->trace_grid * (c->serial ? 100 : WF_TRACE_GRID_PCT) / 100;
     return WF_TRACE_PATHS_PER_BLOCK
                ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + WF_TRACE_PATHS_PER_BLOCK - 1) / WF_TRACE_PATHS_PER_BLOCK))
                : (unsigned)gmax;
@@ -371,7 +372,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     if (per_frame > (size_t)WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: frame too large for one batch");
     const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
     const uint32_t chunk = nf < fit ? nf : fit;
-    const unsigned npipes = per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small : WF_PIPES_LARGE;
+    const unsigned npipes = c->serial ? 1u
+                          : per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small : WF_PIPES_LARGE;
     const unsigned pi = c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;
     pnrt_ctx::Pipe& P = c->pipe[pi];
@@ -544,10 +546,13 @@ int pnrt_set_stream(pnrt_ctx* c, void* s) {
 int pnrt_set_options(pnrt_ctx* c, int options) {
     if (!c) return PNRT_E_ARG;
     int mode = options & 0xff;
-    if ((mode != PNRT_TRAVERSE_EXACT && mode != PNRT_TRAVERSE_ZCULL) || (options & ~0x1ff))
+    if ((mode != PNRT_TRAVERSE_EXACT && mode != PNRT_TRAVERSE_ZCULL) || (options & ~0x3ff))
         return set_err(c, PNRT_E_ARG, "unknown option bits");
     c->mode = mode;
     c->kernel = (options & PNRT_KERNEL_V1) ? 1 : 3;
+    const bool serial = (options & PNRT_SERIAL) != 0;
+    if (serial != c->serial) HIPCHK(c, sync_all(c));   // the pipe rotation restarts from an idle context
+    c->serial = serial;
     return PNRT_OK;
 }
 

@@ -19,6 +19,7 @@ packing loops (main.cpp:409-524)       :class:`PackedScene`
 from __future__ import annotations
 
 import ctypes
+import time
 import dataclasses
 from typing import Sequence
 
@@ -198,6 +199,11 @@ class PackedScene:
     lights: np.ndarray       # (nl, 3)
     lights_sum_area: float
     max_depth: int
+    # BuildBVH's input (per-triangle Bound + boundCenter, (n, 9)) and how long the
+    # build took (seconds; host pnrt_scene_build or GPU pnrt_bvh_build incl. PCIe)
+    tri_bounds: np.ndarray | None = None
+    bvh_seconds: float = 0.0
+    bvh_by: str = "host"
 
     def arrays(self):
         return self.vertices, self.materials, self.triangles, self.nodes, self.lights
@@ -251,13 +257,17 @@ class SceneBuilder:
         """BuildBVH + light list + packing.  With ``bvh_tracer`` (a
         :class:`pnraytracing_amd.tracer.PathTracer`) the BVH is built on its GPU
         (pnrt_bvh_build) -- the same arrays as the host build, bit for bit."""
+        tb = self.tri_bounds()
+        t = time.perf_counter()
         if bvh_tracer is None:
             _check(self._lib.pnrt_scene_build(self._s), "scene_build")
         else:
-            nodes, order, depth = bvh_tracer.build_bvh(self.tri_bounds())
+            nodes, order, depth = bvh_tracer.build_bvh(tb)
             _check(self._lib.pnrt_scene_set_bvh(self._s, N.iptr(order), N.fptr(nodes), len(nodes), depth),
                    "scene_set_bvh")
-        return self._pack()
+        dt = time.perf_counter() - t
+        return dataclasses.replace(self._pack(), tri_bounds=tb, bvh_seconds=dt,
+                                   bvh_by="host" if bvh_tracer is None else "gpu")
 
     def _pack(self) -> PackedScene:
         info = N.SceneInfo()

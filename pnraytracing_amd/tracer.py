@@ -17,6 +17,7 @@ from .host import PackedScene
 TRAVERSE_EXACT = 0
 TRAVERSE_ZCULL = 1
 KERNEL_V1 = 0x100      # | with a traverse mode: one-lane-per-pixel A/B baseline kernel
+SERIAL = 0x200         # | measurement: one call in flight, full trace grid (exclusive kernel times)
 
 
 class PnrtError(RuntimeError):
@@ -163,6 +164,10 @@ class PathTracer:
         p = N.Profile()
         self._ck(self._lib.pnrt_profile_read(self._ctx, ctypes.byref(p)), "pnrt_profile_read")
         return {k: (p.ms[i], int(p.launches[i])) for i, k in enumerate(N.K_CLASSES)}
+
+    def version(self) -> str:
+        """pnrt_version(): library version + sha256 of the device sources it was built from."""
+        return self._lib.pnrt_version().decode()
 
     def debug_math(self, fn: int, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:
         a = np.ascontiguousarray(a, np.float32)
