@@ -26,7 +26,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PNRT_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SRCS = ["pnrt_device.hip"]
-DEVICE_DEPS = ["pnrt_device.hip", "pt_common.h", "pt_kernel.h", "pt_shade.h", "pt_path.h", "pt_passes.h", "pt_wf.h",
+DEVICE_DEPS = ["pnrt_device.hip", "pt_diag.h", "pt_common.h", "pt_kernel.h", "pt_shade.h", "pt_path.h", "pt_passes.h", "pt_wf.h",
                "pt_env.h", "pt_bvh.h", "pn_math.h", "sobol_v.inc"]
 
 

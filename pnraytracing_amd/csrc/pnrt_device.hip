@@ -460,7 +460,10 @@ extern "C" {
 #endif
 // the build stamps the sha256 of the device sources (pnraytracing_amd/build.py),
 // so a stale prebuilt library shipped beside newer sources is detectable
-const char* pnrt_version(void) { return "pnrt-mi355x 0.2 (gfx950) src " PNRT_SRC_HASH; }
+const char* pnrt_version(void) {
+    return PNRT_IS_DIAG_BUILD ? "pnrt-mi355x 0.2 (gfx950) DIAGNOSTIC BUILD src " PNRT_SRC_HASH
+                              : "pnrt-mi355x 0.2 (gfx950) src " PNRT_SRC_HASH;
+}
 
 int pnrt_create(int device, pnrt_ctx** out) {
     if (!out) return PNRT_E_ARG;

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "pn_math.h"
+#include "pt_diag.h"
 
 // ---- constants (ray_tracing.comp:5-9) ---------------------------------------------
 #define PT_FLOAT_MAX 10000000.0f

@@ -27,9 +27,6 @@ struct Hit {      // Interaction (:60-67) of an accepted triangle
 // Shading data of the accepted triangle (TriangleIntersect :320-355), recomputed
 // from its index: the edge functions do not depend on tMax, so they equal the
 // values computed when the triangle was accepted.
-#ifndef WF_KO_ATTR
-#define WF_KO_ATTR 0    // timing diagnostic: hit attributes without the vertex fetches (wrong images)
-#endif
 // The accepted triangle's records: its 48-B test record (positions, material,
 // texture) and its attribute record (the vertices' normals and uvs, i.e. the
 // values of vertices[tri_idx[tri]], gathered at upload) -- one fetch level.

@@ -84,9 +84,6 @@ PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
 // four texels, bit for bit, from one 64-B record instead of two image rows.
 // Left column i0 and right column i1 = clamp(i0 + 1) select record qi = i0 + 1,
 // except at the left edge (i0 = i1 = 0: record 0, both columns 0).
-#ifndef WF_KO_ENV
-#define WF_KO_ENV 0     // timing diagnostics (wrong images): 1 = environment lookups without their
-#endif                  // math or memory reads; 2 = the math, with every tap read from record 0
 #ifndef PT_ENV_QUAD
 #define PT_ENV_QUAD 1
 #endif

@@ -544,24 +544,12 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return (t1 >= t0) & !(r.cull_ok() & (hi <= 0.0f));
 }
 
-#ifndef WF_DIAG_NOSTORE
-#define WF_DIAG_NOSTORE 0   // timing experiment: drop the trace results (wrong images)
-#endif
-#ifndef WF_DIAG_VALU
-#define WF_DIAG_VALU 0      // timing diagnostic: extra VALU instructions per traversal step
-#endif
-#ifndef WF_STATS
-#define WF_STATS 0          // diagnostic builds: count iterations / lane steps per trace launch
-#endif
 #ifndef WF_SUB
 #define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
 #endif
 #define WF_NSUB (256 / WF_SUB)
 #ifndef WF_KIND_ORDER
 #define WF_KIND_ORDER 0x210 // sweep order of the ray kinds, one hex digit each (0 light, 1 env, 2 continuation)
-#endif
-#ifndef WF_TIMING
-#define WF_TIMING 0         // diagnostic builds: per-wave timestamps of the trace kernel
 #endif
 
 PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
