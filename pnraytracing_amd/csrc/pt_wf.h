@@ -59,6 +59,41 @@
 #define WF_NQUEUED (WF_QUEUED(0) + WF_QUEUED(1) + WF_QUEUED(2))
 PN_DEV constexpr uint32_t wf_qidx(int k) { return (k > 0 && WF_QUEUED(0)) + (k > 1 && WF_QUEUED(1)); }
 
+// Cache policy of the streamed path-state traffic (path state, ray records,
+// frame colours): written once by a setup, read once by the trace and the next
+// shade, never by the same CU's L2 while the line could still be there -- 1 GB
+// per state set, far beyond the 4 MB L2 of an XCD, which the trace kernels of
+// the calls in flight use for the BVH.  WF_LD_POLICY = 1: non-temporal loads
+// (C2 +0.5 to +1.2 %, same box).  WF_ST_POLICY = buffer-store aux bits: 0 plain
+// (kept), 16 = sc1 (write-through, the line leaves the XCD's L2: -4 %), 2 = nt
+// (neutral).
+#ifndef WF_ST_POLICY
+#define WF_ST_POLICY 0
+#endif
+#ifndef WF_LD_POLICY
+#define WF_LD_POLICY 1
+#endif
+PN_DEV void ps_st(float4* base, size_t i, float4 v) {
+    if constexpr (WF_ST_POLICY == 0) {
+        base[i] = v;
+    } else {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+        u4 d;
+        d.x = __float_as_uint(v.x); d.y = __float_as_uint(v.y); d.z = __float_as_uint(v.z); d.w = __float_as_uint(v.w);
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)(i * 16u), 0, WF_ST_POLICY);
+    }
+}
+PN_DEV float4 ps_ld(const float4* p) {
+#if WF_LD_POLICY == 0
+    return *p;
+#else
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#endif
+}
+
 // ray kinds a setup emitted (enqueue) ...
 #define WF_RLIGHT 2u
 #define WF_RENV 4u
@@ -156,7 +191,7 @@ PN_DEV uint32_t wf_block_rank(bool live, uint32_t& total) {
 
 PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
     color = mk3(clampf(color.x, 0.f, 1.f), clampf(color.y, 0.f, 1.f), clampf(color.z, 0.f, 1.f));
-    colors[((size_t)k * fp.rows + lr) * fp.width + x] = make_float4(color.x, color.y, color.z, 0.f);
+    ps_st(colors, ((size_t)k * fp.rows + lr) * fp.width + x, make_float4(color.x, color.y, color.z, 0.f));
 }
 
 // Path state a bounce's setup starts from (in registers: the fused kernels
@@ -279,13 +314,13 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         f3 lightBRDF = disney(bc, lightL);
         LD = divs(muls(mul(lightBRDF, lf.li), pnm_fabs(dot(N, lightL))), pl);
         rays.dL = ldir;
-        if (WF_LIGHT_FROM_STATE) w.P7[i] = make_float4(ldir.x, ldir.y, ldir.z, 0.f);
+        if (WF_LIGHT_FROM_STATE) ps_st(w.P7, i, make_float4(ldir.x, ldir.y, ldir.z, 0.f));
         nfl |= WF_RLIGHT;
     }
     // stored as soon as final (shorter live ranges), and only when shade can use it:
     // shade takes (0, 0) for a path without a light ray, as the reference's
     // initial LDirect / lightPDF (:878-879)
-    if (nfl & WF_RLIGHT) w.P3[i] = make_float4(LD.x, LD.y, LD.z, pl);
+    if (nfl & WF_RLIGHT) ps_st(w.P3, i, make_float4(LD.x, LD.y, LD.z, pl));
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -301,7 +336,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
-    if (nfl & WF_RENV) w.P4[i] = make_float4(LE.x, LE.y, LE.z, 0.f);
+    if (nfl & WF_RENV) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -352,11 +387,11 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     rays.oOff = add(P, muls(N, 0.0001f));
     const uint32_t meta = slot | ((nfl & WF_RLIGHT) ? WF_META_RL : 0u) | ((nfl & WF_RENV) ? WF_META_RE : 0u) |
                           ((uint32_t)bounce << WF_META_BSHIFT);
-    w.P0[i] = make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF);
-    w.P1[i] = make_float4(L.x, L.y, L.z, NdotL);
-    w.P2[i] = make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe);
-    w.P5[i] = make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed));
-    w.P6[i] = make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(meta));
+    ps_st(w.P0, i, make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF));
+    ps_st(w.P1, i, make_float4(L.x, L.y, L.z, NdotL));
+    ps_st(w.P2, i, make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe));
+    ps_st(w.P5, i, make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed)));
+    ps_st(w.P6, i, make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(meta)));
     return nfl | WF_RCONT;
 }
 
@@ -417,8 +452,8 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
             const size_t slot = (size_t)wf_qidx(k) * b.npad + (size_t)blockIdx.x * 256 + bin[k][oct[k]] + rank[k];
             const f3 o = k == 1 ? rays.oP : rays.oOff;
             const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
-            b.rayO[slot] = make_float4(o.x, o.y, o.z, __uint_as_float(i));
-            b.rayD[slot] = make_float4(d.x, d.y, d.z, 0.f);
+            ps_st(b.rayO, slot, make_float4(o.x, o.y, o.z, __uint_as_float(i)));
+            ps_st(b.rayD, slot, make_float4(d.x, d.y, d.z, 0.f));
         }
     }
 }
@@ -527,12 +562,10 @@ PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa) {
 // BoundIntersect (:213-228) for traversal decisions.  fminf/fmaxf (v_min/v_max)
 // drop NaNs exactly like the oracle's min/max; the results only feed
 // comparisons, where the sign of a zero cannot matter -> same booleans.
-// Returns the box's z-slab lower end (zlo) in the triangle test's frame.
+// box_slabs takes the six slab distances (far x y z, near x y z) and returns the
+// box's z-slab lower end (zlo) in the triangle test's frame.
 template <bool IDENT = false>
-PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
-                     float& zlo) {
-    float fx = (mxx - r.o.x) * r.inv.x, fy = (mxy - r.o.y) * r.inv.y, fz = (mxz - r.o.z) * r.inv.z;
-    float nx = (mnx - r.o.x) * r.inv.x, ny = (mny - r.o.y) * r.inv.y, nz = (mnz - r.o.z) * r.inv.z;
+PN_DEV bool box_slabs(const RayP& r, float fx, float fy, float fz, float nx, float ny, float nz, float& zlo) {
     float t1 = fminf(fmaxf(fx, nx), fminf(fmaxf(fy, ny), fmaxf(fz, nz)));
     float t0 = fmaxf(fminf(fx, nx), fmaxf(fminf(fy, ny), fminf(fz, nz)));
     const int kz = IDENT ? 2 : r.kz();
@@ -542,6 +575,13 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     zlo = lo;
     // zhi <= 0: the whole box is behind the ray in the triangle test's frame
     return (t1 >= t0) & !(r.cull_ok() & (hi <= 0.0f));
+}
+template <bool IDENT = false>
+PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                     float& zlo) {
+    float fx = (mxx - r.o.x) * r.inv.x, fy = (mxy - r.o.y) * r.inv.y, fz = (mxz - r.o.z) * r.inv.z;
+    float nx = (mnx - r.o.x) * r.inv.x, ny = (mny - r.o.y) * r.inv.y, nz = (mnz - r.o.z) * r.inv.z;
+    return box_slabs<IDENT>(r, fx, fy, fz, nx, ny, nz, zlo);
 }
 
 #ifndef WF_SUB
@@ -645,7 +685,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
     const float4* O = fromState ? b.wr.P0 : b.rayO;
     const float4* D = fromState ? (kind == 0 ? b.wr.P7 : b.wr.P1) : b.rayD;
     const uint32_t at = fromState ? e : ri;
-    const float4 ro = O[at], rd = D[at];
+    const float4 ro = ps_ld(O + at), rd = ps_ld(D + at);
     p = fromState ? e : __float_as_uint(ro.w);
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
@@ -823,7 +863,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
                           float4* colors, uint32_t i, PathIn& q, int& bounce, uint32_t& slot, int& x, int& py,
                           uint32_t& frame) {
     const PathSet& rd = b.rd;
-    const float4 p0 = rd.P0[i], p1 = rd.P1[i], p2 = rd.P2[i], p5 = rd.P5[i], p6 = rd.P6[i];
+    const float4 p0 = ps_ld(rd.P0 + i), p1 = ps_ld(rd.P1 + i), p2 = ps_ld(rd.P2 + i), p5 = ps_ld(rd.P5 + i),
+                 p6 = ps_ld(rd.P6 + i);
     const int ht = b.hit[i];
     // the light / env candidates are read only where they count: an occluded
     // light ray zeroes LDirect and lightPDF (:890), an occluded or absent env ray
@@ -836,8 +877,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     slot = meta & WF_META_SLOT;
     const bool useL = (meta & WF_META_RL) && !(oc & 0xffu);
     const bool useE = (meta & WF_META_RE) && !(oc >> 8);
-    const float4 p3 = *(useL ? rd.P3 + i : s.zero4);
-    const float4 p4 = *(useE ? rd.P4 + i : s.zero4);
+    const float4 p3 = ps_ld(useL ? rd.P3 + i : s.zero4);
+    const float4 p4 = ps_ld(useE ? rd.P4 + i : s.zero4);
     // the continuation hit's records, in flight while the MIS sum waits for P3/P4
     // (a miss reads triangle 0's, unused)
     const HitFetch hf = hit_fetch(s, ht < 0 ? 0 : ht);

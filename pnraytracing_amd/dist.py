@@ -31,8 +31,12 @@ BAND = 8
 class ShardedFrame:
     """Render the rows of this rank and gather the frame to rank 0."""
 
-    def __init__(self, tracer, band: int = BAND, device: str | torch.device = "cuda", group=None):
+    def __init__(self, tracer, band: int = BAND, device: str | torch.device = "cuda", group=None,
+                 collective: bool = False):
         self.tracer, self.band, self.group = tracer, band, group
+        # collective=True: gather through the process group even with one rank (the
+        # RCCL path exercised on a one-GPU box; the image is the same either way)
+        self.collective = collective and dist.is_initialized()
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.device = torch.device(device)
@@ -86,7 +90,7 @@ class ShardedFrame:
         (row 0 = bottom) on rank 0 and None elsewhere."""
         if self.my_rows:
             self.tracer.pack_rows(self.send.data_ptr(), self.band, self.world, self.rank)
-        if self.world == 1:
+        if self.world == 1 and not self.collective:
             self.image.copy_(self.send)
             return self.image
         send = self.send.cpu() if self.stage else self.send
@@ -126,7 +130,7 @@ class ShardedFrame:
         render stream wait for it: the next frames render while the rows travel
         over xGMI.  Double-buffered; :meth:`finish` completes the last gather and
         assembles the image on rank 0.  (Synchronous for one rank / gloo staging.)"""
-        if self.world == 1 or self.stage:
+        if (self.world == 1 and not self.collective) or self.stage:
             self._last = self._gather()
             return
         slot = self._slot
@@ -142,7 +146,7 @@ class ShardedFrame:
 
     def _finish(self) -> torch.Tensor | None:
         """Complete the outstanding gathers; rank 0 gets the newest frame's image."""
-        if self.world == 1 or self.stage:
+        if (self.world == 1 and not self.collective) or self.stage:
             return self._last
         for slot in (self._newest ^ 1, self._newest):
             if self._work[slot] is not None:

@@ -25,3 +25,45 @@ def test_two_ranks_gather_equals_one(tmp_path):
                    stdout=subprocess.DEVNULL)
     x, y = np.load(a), np.load(b)
     assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def _single_rank_c4(path):
+    from pnraytracing_amd import scenes
+    from pnraytracing_amd.tracer import PathTracer
+    cfg = scenes.teapot_c4(320, 176)
+    with PathTracer(0) as pt:
+        pt.load(cfg)
+        for k in range(3):
+            pt.render(4 * k, 4)
+        return pt.read_accum()
+
+
+def _run_worker(tmp_path, nproc, port):
+    out = str(tmp_path / f"rccl{nproc}.npy")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "tests/rccl_worker.py", out],
+                       cwd=REPO, env=env, timeout=300, capture_output=True, text=True)
+    return r, out
+
+
+def test_rccl_gather_one_rank(tmp_path):
+    """The RCCL gather path of ShardedFrame (dist.gather on device tensors, async,
+    double-buffered) executed with one rank: image = the plain render."""
+    r, out = _run_worker(tmp_path, 1, 29551)
+    assert r.returncode == 0, r.stderr[-3000:]
+    x, y = _single_rank_c4(None), np.load(out)
+    assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_rccl_gather_two_ranks_one_gpu(tmp_path):
+    """Two RCCL ranks on the box's one GPU, when RCCL accepts that (it may refuse a
+    duplicate device): the gathered bands = the single-rank image."""
+    r, out = _run_worker(tmp_path, 2, 29553)
+    if r.returncode != 0:
+        msg = r.stderr[-3000:]
+        if "uplicate GPU" in msg or "invalid usage" in msg.lower():
+            pytest.skip("RCCL refuses two ranks on one GPU: " + msg.strip().splitlines()[-1][:200])
+        raise AssertionError(msg)
+    x, y = _single_rank_c4(None), np.load(out)
+    assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
