@@ -178,7 +178,9 @@ static int prof_collect(pnrt_ctx* c) {
     return PNRT_OK;
 }
 
-#define WF_MAX_CHUNK_FRAMES 8
+#ifndef WF_MAX_CHUNK_FRAMES
+#define WF_MAX_CHUNK_FRAMES 8    // frames per batch at most (a 4-spp call is one batch)
+#endif
 
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
@@ -290,7 +292,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
         // segment dequeue counter (+ the WF_STATS census)
         // (zeroed by the setup kernel that queued the rays; the census builds also memset)
-        if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 256, st));
+        if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(trace_grid_for(c, b.n)), dim3(WF_TRACE_BLOCK), 0, st, s, b,
@@ -317,9 +319,14 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
                     us(tend));
         }
         if (WF_STATS) {
-            unsigned long long stt[8];
+            unsigned long long stt[8 + 48];
             HIPCHK(c, hipStreamSynchronize(st));
             HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
+            for (int k = 0; k < 3; ++k) {        // lane steps per ray, log2 buckets, by ray kind
+                fprintf(stderr, "[trace hist] bounce %d kind %d:", bounce, k);
+                for (int q = 0; q < 16; ++q) fprintf(stderr, " %llu", stt[8 + 16 * k + q]);
+                fprintf(stderr, "\n");
+            }
             fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu uniform-fetch iters=%llu "
                     "refills=%llu rays=%llu  lane-steps/ray=%.1f  continuation lane-steps=%.1f%%\n", bounce, b.n, stt[0],
                     stt[0] ? (double)stt[1] / stt[0] : 0.0, stt[2], stt[3], stt[4], stt[5], stt[6],

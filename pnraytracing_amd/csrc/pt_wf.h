@@ -605,6 +605,7 @@ struct TravState {
     int hitTri, lt, lc;       // accepted triangle; pending triangle range [lt, lt + lc)
     uint32_t spa, cur;        // stack position (see wf_push); node to visit next
     bool any;                 // any-hit (shadow) ray
+    uint32_t nst;             // WF_STATS builds: lane steps of this ray
 };
 
 // One traversal step of a lane's ray; returns true when the ray is finished
@@ -720,6 +721,12 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     // 256 neighbouring paths, kind-major); one atomic per segment
     const uint32_t nseg = 3u * b.nseg_k * WF_NSUB;
     uint64_t t_start = WF_TIMING ? __builtin_amdgcn_s_memrealtime() : 0, t_exh = 0;
+    // WF_STATS: per ray kind, a histogram of lane steps per ray (bucket = floor(log2(steps)))
+    __shared__ unsigned int hist[WF_STATS ? 3 * 16 : 1];
+    if (WF_STATS) {
+        if (threadIdx.x < 48) hist[threadIdx.x] = 0u;
+        __syncthreads();
+    }
     uint32_t n_rays = 0;
     uint32_t next = 0, end = 0, ckind = 0, qpart = 0;
     bool exhausted = false;
@@ -793,6 +800,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     }
                     t.r = nr; t.tMax = ntmax; t.any = nany; rid = (kind << 30) | p;
                     t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
+                    t.nst = 0;
                     busy = 1;
                 }
             }
@@ -825,6 +833,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 }
                 if (busy) {
                     const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
+                    if (WF_STATS) {
+                        t.nst += 1;
+                        if (done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
+                    }
                     if (done) {
                         const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
                         if (!WF_DIAG_NOSTORE) {
@@ -851,6 +863,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     if (WF_TIMING && lane == 0) {      // diagnostic builds: per-wave start / queue-empty / end (100 MHz clock)
         unsigned long long* t = b.stats + 8 + 4 * ((size_t)blockIdx.x * (WF_TRACE_BLOCK / 64) + (threadIdx.x >> 6));
         t[0] = t_start; t[1] = t_exh; t[2] = __builtin_amdgcn_s_memrealtime(); t[3] = 0;
+    }
+    if (WF_STATS) {
+        __syncthreads();
+        if (threadIdx.x < 48 && hist[threadIdx.x]) atomicAdd(b.stats + 8 + threadIdx.x, (unsigned long long)hist[threadIdx.x]);
     }
     if (WF_STATS && lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd(b.stats + k, st[k]);
