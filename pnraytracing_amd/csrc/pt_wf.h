@@ -742,44 +742,88 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     int busy = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
 
+    // dequeue the wave's next queue item into [next, end) / ckind, or set `exhausted`
+    // (wave-uniform; lane 0 issues the atomic)
+    auto dequeue = [&]() {
+        // WF_QSHARDS dequeue counters, item i on counter i % WF_QSHARDS: the
+        // blocks sharing an XCD (blockIdx % 8) start on their own counter and
+        // move on when it runs dry, so the global sweep order is unchanged
+        // while each counter sees 1/WF_QSHARDS of the device-scope atomics
+        uint32_t seg = nseg;
+        for (;;) {
+            const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
+            t = __builtin_amdgcn_readfirstlane(t);
+            const uint32_t item = t * WF_QSHARDS + p;
+            if (item < nseg) { seg = item; break; }
+            if (++qpart == WF_QSHARDS) break;
+        }
+        if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
+        else {
+            // one dequeue = WF_SUB rays of a segment (finer grains balance the
+            // drain at the end of the launch).  Kind order of the sweep
+            // (WF_KIND_ORDER): continuation rays (closest hit, the longest
+            // traversals) first, then env shadow rays, so the launch ends
+            // on the short light shadow rays
+            const uint32_t sj = seg / WF_NSUB, part = seg - sj * WF_NSUB;
+            const uint32_t qk = sj / b.nseg_k;
+            const uint32_t j = sj - qk * b.nseg_k;
+            ckind = (uint32_t)(WF_KIND_ORDER >> (4 * (2 - (int)qk))) & 0xfu;
+            const uint32_t cnt = b.segcount[ckind * b.nseg_k + j];
+            const uint32_t lo = min(part * (uint32_t)WF_SUB, cnt);
+            next = ckind * b.npad + j * 256u + lo;
+            end = ckind * b.npad + j * 256u + min(lo + (uint32_t)WF_SUB, cnt);
+        }
+    };
+    // one traversal step of a busy lane, the result stored when its ray is done
+    auto step_lane = [&](auto ident_tag) {
+        constexpr bool ID = decltype(ident_tag)::value;
+        if (WF_STATS) {
+            st[0] += 1;
+            st[1] += __popcll(__ballot(busy != 0));
+            st[2] += __popcll(__ballot(busy != 0 && t.lc > 0));
+            st[3] += __popcll(__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE));
+            st[7] += __popcll(__ballot(busy != 0 && (rid >> 30) == 2u));     // continuation-ray lane steps
+            {   // steps whose fetch address is the same for every active lane
+                const uint64_t act = __ballot(busy != 0);
+                const uint32_t fo = t.lc > 0 ? 0x80000000u + (uint32_t)t.lt : t.cur;
+                const uint32_t f0 = __shfl(fo, act ? __ffsll((long long)act) - 1 : 0);
+                st[4] += (act != 0 && __ballot(busy != 0 && fo != f0) == 0) ? 1 : 0;
+            }
+        }
+        if (busy) {
+            const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
+            if (WF_STATS) {
+                t.nst += 1;
+                if (done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
+            }
+            if (done) {
+                const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
+                if (!WF_DIAG_NOSTORE) {
+                    if (kind == 2) b.hit[p] = t.hitTri;
+                    else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
+                }
+                busy = 0;
+            }
+        }
+#if WF_DIAG_VALU
+        {   // timing diagnostic: extra VALU per iteration (is the loop issue-bound?)
+            float d = __int_as_float(t.lt);
+#pragma unroll
+            for (int q = 0; q < WF_DIAG_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
+            t.lt = __float_as_int(d) == 0x7fffffff ? 0 : t.lt;
+        }
+#endif
+    };
+
     for (;;) {
         // ---- refill: idle lanes take the wave's next queued rays; more passes when a
         // segment runs out part-way (wave-uniform control flow only)
         const int busy0 = WF_STATS ? __popcll(__ballot(busy != 0)) : 0;
         auto refill = [&]() {
             const uint64_t idle = __ballot(busy == 0);
-            if (idle != 0 && next >= end && !exhausted) {
-                // WF_QSHARDS dequeue counters, item i on counter i % WF_QSHARDS: the
-                // blocks sharing an XCD (blockIdx % 8) start on their own counter and
-                // move on when it runs dry, so the global sweep order is unchanged
-                // while each counter sees 1/WF_QSHARDS of the device-scope atomics
-                uint32_t seg = nseg;
-                for (;;) {
-                    const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
-                    uint32_t t = 0;
-                    if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
-                    t = __builtin_amdgcn_readfirstlane(t);
-                    const uint32_t item = t * WF_QSHARDS + p;
-                    if (item < nseg) { seg = item; break; }
-                    if (++qpart == WF_QSHARDS) break;
-                }
-                if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
-                else {
-                    // one dequeue = WF_SUB rays of a segment (finer grains balance the
-                    // drain at the end of the launch).  Kind order of the sweep
-                    // (WF_KIND_ORDER): continuation rays (closest hit, the longest
-                    // traversals) first, then env shadow rays, so the launch ends
-                    // on the short light shadow rays
-                    const uint32_t sj = seg / WF_NSUB, part = seg - sj * WF_NSUB;
-                    const uint32_t qk = sj / b.nseg_k;
-                    const uint32_t j = sj - qk * b.nseg_k;
-                    ckind = (uint32_t)(WF_KIND_ORDER >> (4 * (2 - (int)qk))) & 0xfu;
-                    const uint32_t cnt = b.segcount[ckind * b.nseg_k + j];
-                    const uint32_t lo = min(part * (uint32_t)WF_SUB, cnt);
-                    next = ckind * b.npad + j * 256u + lo;
-                    end = ckind * b.npad + j * 256u + min(lo + (uint32_t)WF_SUB, cnt);
-                }
-            }
+            if (idle != 0 && next >= end && !exhausted) dequeue();
             if (idle != 0 && next < end) {
                 const uint32_t myid = next + lanes_below(idle);
                 next = min(next + (uint32_t)__popcll(idle), end);
@@ -816,44 +860,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------
         // (IDENT: no lane of the wave needs the triangle test's axis permutation)
         auto run = [&](auto ident_tag) {
-            constexpr bool ID = decltype(ident_tag)::value;
             for (;;) {
-                if (WF_STATS) {
-                    st[0] += 1;
-                    st[1] += __popcll(__ballot(busy != 0));
-                    st[2] += __popcll(__ballot(busy != 0 && t.lc > 0));
-                    st[3] += __popcll(__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE));
-                    st[7] += __popcll(__ballot(busy != 0 && (rid >> 30) == 2u));     // continuation-ray lane steps
-                    {   // steps whose fetch address is the same for every active lane
-                        const uint64_t act = __ballot(busy != 0);
-                        const uint32_t fo = t.lc > 0 ? 0x80000000u + (uint32_t)t.lt : t.cur;
-                        const uint32_t f0 = __shfl(fo, act ? __ffsll((long long)act) - 1 : 0);
-                        st[4] += (act != 0 && __ballot(busy != 0 && fo != f0) == 0) ? 1 : 0;
-                    }
-                }
-                if (busy) {
-                    const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
-                    if (WF_STATS) {
-                        t.nst += 1;
-                        if (done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
-                    }
-                    if (done) {
-                        const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
-                        if (!WF_DIAG_NOSTORE) {
-                            if (kind == 2) b.hit[p] = t.hitTri;
-                            else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
-                        }
-                        busy = 0;
-                    }
-                }
-#if WF_DIAG_VALU
-                {   // timing diagnostic: extra VALU per iteration (is the loop issue-bound?)
-                    float d = __int_as_float(t.lt);
-#pragma unroll
-                    for (int q = 0; q < WF_DIAG_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
-                    t.lt = __float_as_int(d) == 0x7fffffff ? 0 : t.lt;
-                }
-#endif
+                step_lane(ident_tag);
                 if (__popcll(__ballot(busy != 0)) <= thr) break;
             }
         };
