@@ -1,6 +1,6 @@
 """Per-rank throughput of the N-GPU row-band split, measured on one GPU: render only
 shard 0 of N (what rank 0 does at N GPUs, without the gather) and report the implied
-whole-node rate N x per-rank.  python tools/shard_sim.py [steps]"""
+whole-node rate N x per-rank.  python tools/shard_sim.py [steps] [frames per call]"""
 import os
 import sys
 import time
@@ -13,19 +13,20 @@ from pnraytracing_amd import scenes  # noqa: E402
 from pnraytracing_amd.tracer import PathTracer, shard_rows  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+fpc = int(sys.argv[2]) if len(sys.argv) > 2 else 4      # frames per pnrt_render call (4 = one 4-spp step)
 cfg = scenes.bunny_c2()
 with PathTracer(0) as pt:
     pt.load(cfg)
     for n in (1, 2, 4, 8):
         rows = len(shard_rows(cfg.height, 8, n, 0))
         for k in range(3):
-            pt.render(4 * k, 4, 8, n, 0)
+            pt.render(fpc * k, fpc, 8, n, 0)
         pt.synchronize()
         t = time.perf_counter()
         for k in range(steps):
-            pt.render(4 * (3 + k), 4, 8, n, 0)
+            pt.render(fpc * (3 + k), fpc, 8, n, 0)
         pt.synchronize()
         dt = (time.perf_counter() - t) / steps
-        per_rank = rows * cfg.width * 4 / dt / 1e6
+        per_rank = rows * cfg.width * fpc / dt / 1e6
         print(f"N={n}: rank-0 rows {rows}, {dt * 1e3:.3f} ms/step, {per_rank:.1f} Msamples/s per rank, "
               f"implied node {per_rank * n:.1f} (efficiency vs N=1 in the last column)", flush=True)
