@@ -300,7 +300,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         }
         HIPCHK(c, hipGetLastError());
         if (WF_TIMING) {   // tail census: when the queue ran dry vs when the last wave ended
-            const size_t nw = (size_t)c->trace_grid * (WF_TRACE_BLOCK / 64);
+            const size_t nw = (size_t)trace_grid_for(c, b.n) * (WF_TRACE_BLOCK / 64);   // waves launched
             std::vector<unsigned long long> t(4 * nw);
             HIPCHK(c, hipStreamSynchronize(st));
             HIPCHK(c, hipMemcpy(t.data(), b.stats + 8, t.size() * 8, hipMemcpyDeviceToHost));
@@ -317,6 +317,19 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             fprintf(stderr, "[trace timing] bounce %d n=%u first-empty %.1f us, wave ends p10 %.1f p50 %.1f p90 %.1f "
                     "max %.1f us\n", bounce, b.n, us(tex), us(ends[nw / 10]), us(ends[nw / 2]), us(ends[nw * 9 / 10]),
                     us(tend));
+            // the slowest 1 % of waves: end time and their longest last ray (kind, lane steps)
+            std::vector<std::pair<unsigned long long, unsigned long long>> we;
+            std::vector<unsigned long long> wx;
+            for (size_t w = 0; w < nw; ++w) we.push_back({t[4 * w + 2], w});
+            std::sort(we.begin(), we.end());
+            fprintf(stderr, "[trace tail] bounce %d (end us, kind/lane steps of the last ray, iterations and us after the queue ran dry):", bounce);
+            for (size_t q = nw - std::max<size_t>(1, nw / 100); q < nw; q += std::max<size_t>(1, nw / 1000)) {
+                const size_t w = we[q].second;
+                const unsigned long long c = t[4 * w + 3];
+                fprintf(stderr, " %.0f:k%llu/%llu:%llu/%.0f", us(t[4 * w + 2]), (c >> 16) & 0xffff, c & 0xffff, c >> 32,
+                        (double)(t[4 * w + 2] - t[4 * w + 1]) / 100.0);
+            }
+            fprintf(stderr, "\n");
         }
         if (WF_STATS) {
             unsigned long long stt[8 + 48];

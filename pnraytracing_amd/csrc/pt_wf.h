@@ -740,6 +740,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     t.any = true;
     uint32_t rid = 0;
     int busy = 0;
+    uint64_t last_ray = 0;      // WF_TIMING builds: (iteration, kind, lane steps) of the lane's last finished ray
+    uint32_t witer = 0, witer_exh = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
 
     // dequeue the wave's next queue item into [next, end) / ckind, or set `exhausted`
@@ -759,10 +761,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (item < nseg) { seg = item; break; }
             if (++qpart == WF_QSHARDS) break;
         }
-        if (seg >= nseg) { exhausted = true; if (WF_TIMING) t_exh = __builtin_amdgcn_s_memrealtime(); }
+        if (seg >= nseg) { exhausted = true; if (WF_TIMING) { t_exh = __builtin_amdgcn_s_memrealtime(); witer_exh = witer; } }
         else {
-            // one dequeue = WF_SUB rays of a segment (finer grains balance the
-            // drain at the end of the launch).  Kind order of the sweep
+            // one dequeue = WF_SUB rays of a segment.  Kind order of the sweep
             // (WF_KIND_ORDER): continuation rays (closest hit, the longest
             // traversals) first, then env shadow rays, so the launch ends
             // on the short light shadow rays
@@ -792,12 +793,12 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 st[4] += (act != 0 && __ballot(busy != 0 && fo != f0) == 0) ? 1 : 0;
             }
         }
+        if (WF_TIMING) ++witer;
         if (busy) {
             const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
-            if (WF_STATS) {
-                t.nst += 1;
-                if (done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
-            }
+            if (WF_STATS || WF_TIMING) t.nst += 1;
+            if (WF_STATS && done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
+            if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
                 const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
                 if (!WF_DIAG_NOSTORE) {
@@ -870,7 +871,18 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     }
     if (WF_TIMING && lane == 0) {      // diagnostic builds: per-wave start / queue-empty / end (100 MHz clock)
         unsigned long long* t = b.stats + 8 + 4 * ((size_t)blockIdx.x * (WF_TRACE_BLOCK / 64) + (threadIdx.x >> 6));
-        t[0] = t_start; t[1] = t_exh; t[2] = __builtin_amdgcn_s_memrealtime(); t[3] = 0;
+        t[0] = t_start; t[1] = t_exh; t[2] = __builtin_amdgcn_s_memrealtime();
+        t[3] = 0;
+    }
+    if (WF_TIMING) {    // the wave's last ray to finish: kind << 16 | its lane steps (max over the wave's lanes)
+        uint64_t lr = last_ray;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t v = ((uint64_t)__shfl_xor((unsigned)(lr >> 32), o) << 32) | (unsigned)__shfl_xor((unsigned)lr, o);
+            lr = v > lr ? v : lr;
+        }
+        if (lane == 0)
+            b.stats[8 + 4 * ((size_t)blockIdx.x * (WF_TRACE_BLOCK / 64) + (threadIdx.x >> 6)) + 3] =
+                (uint64_t)(witer - witer_exh) << 32 | (lr & 0xffffffffu);
     }
     if (WF_STATS) {
         __syncthreads();
