@@ -584,6 +584,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return box_slabs<IDENT>(r, fx, fy, fz, nx, ny, nz, zlo);
 }
 
+#ifndef WF_BLOCKQ
+#define WF_BLOCKQ 1         // block-level ray queue shared by a block's waves (see the trace kernel)
+#endif
 #ifndef WF_SUB
 #define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
 #endif
@@ -777,6 +780,68 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             end = ckind * b.npad + j * 256u + min(lo + (uint32_t)WF_SUB, cnt);
         }
     };
+#if WF_BLOCKQ
+    // Block-level ray queue (WF_BLOCKQ): the block's four waves share one dequeued
+    // segment; a wave claims as many rays as it has idle lanes with an LDS atomic
+    // on bq_claim = (generation << 16 | rays claimed), the segment of generation g
+    // is bq_seg[g & 7] = {first slot, end slot, kind}; the first wave to find it used
+    // up (a compare-and-swap on bq_refill) dequeues the next global segment and
+    // publishes it as generation g + 1, the others sleep until then.  The last
+    // segment of a block is thus worked through by all its waves, not by one.
+    __shared__ uint32_t bq_claim, bq_refill, bq_done;
+    __shared__ uint32_t bq_seg[8][3];
+    if (threadIdx.x == 0) {
+        bq_claim = 0u; bq_refill = 0u; bq_done = 0u;
+        bq_seg[0][0] = bq_seg[0][1] = 0u; bq_seg[0][2] = 0u;
+    }
+    __syncthreads();
+    auto bclaim = [&](uint32_t want) {
+        for (uint32_t guard = 0; guard < (1u << 10); ++guard) {
+            uint32_t c = 0;
+            if (lane == 0) c = __hip_atomic_fetch_add(&bq_claim, want, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            c = __builtin_amdgcn_readfirstlane(c);
+            const uint32_t g = c >> 16, old = c & 0xffffu;
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(bq_seg[g & 7][0]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(bq_seg[g & 7][1]);
+            if (old < hi - lo) {
+                next = lo + old; end = min(next + want, hi);
+                ckind = __builtin_amdgcn_readfirstlane(bq_seg[g & 7][2]);
+                return;
+            }
+            if (__hip_atomic_load(&bq_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) { exhausted = true; return; }
+            uint32_t won = 0;
+            if (lane == 0) {
+                uint32_t e = g;
+                won = __hip_atomic_compare_exchange_strong(&bq_refill, &e, g + 1, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+            }
+            won = __builtin_amdgcn_readfirstlane(won);
+            if (won) {                          // this wave fetches generation g + 1
+                do {
+                    dequeue();
+                } while (!exhausted && next >= end);            // skip empty segments
+                if (lane == 0) {
+                    const uint32_t q = (g + 1) & 7;
+                    bq_seg[q][0] = exhausted ? 0u : next;
+                    bq_seg[q][1] = exhausted ? 0u : end;
+                    bq_seg[q][2] = ckind;
+                    if (exhausted) __hip_atomic_store(&bq_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&bq_claim, (g + 1) << 16, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                exhausted = false;              // re-claimed below (every wave leaves through bq_done)
+                next = end = 0;
+                continue;
+            }
+            // another wave is fetching generation g + 1
+            for (uint32_t w = 0; w < (1u << 16); ++w) {
+                const uint32_t c2 = __hip_atomic_load(&bq_claim, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if ((c2 >> 16) != g) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        exhausted = true;                       // guard: never expected
+    };
+#endif
     // one traversal step of a busy lane, the result stored when its ray is done
     auto step_lane = [&](auto ident_tag) {
         constexpr bool ID = decltype(ident_tag)::value;
@@ -824,7 +889,13 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         const int busy0 = WF_STATS ? __popcll(__ballot(busy != 0)) : 0;
         auto refill = [&]() {
             const uint64_t idle = __ballot(busy == 0);
-            if (idle != 0 && next >= end && !exhausted) dequeue();
+            if (idle != 0 && next >= end && !exhausted) {
+#if WF_BLOCKQ
+                bclaim((uint32_t)__popcll(idle));
+#else
+                dequeue();
+#endif
+            }
             if (idle != 0 && next < end) {
                 const uint32_t myid = next + lanes_below(idle);
                 next = min(next + (uint32_t)__popcll(idle), end);
