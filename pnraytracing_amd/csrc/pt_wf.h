@@ -784,12 +784,12 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     // Block-level ray queue (WF_BLOCKQ): the block's four waves share one dequeued
     // segment; a wave claims as many rays as it has idle lanes with an LDS atomic
     // on bq_claim = (generation << 16 | rays claimed), the segment of generation g
-    // is bq_seg[g & 7] = {first slot, end slot, kind}; the first wave to find it used
+    // is bq_seg[g & 15] = {first slot, end slot, kind}; the first wave to find it used
     // up (a compare-and-swap on bq_refill) dequeues the next global segment and
     // publishes it as generation g + 1, the others sleep until then.  The last
     // segment of a block is thus worked through by all its waves, not by one.
     __shared__ uint32_t bq_claim, bq_refill, bq_done;
-    __shared__ uint32_t bq_seg[8][3];
+    __shared__ uint32_t bq_seg[16][3];
     if (threadIdx.x == 0) {
         bq_claim = 0u; bq_refill = 0u; bq_done = 0u;
         bq_seg[0][0] = bq_seg[0][1] = 0u; bq_seg[0][2] = 0u;
@@ -801,11 +801,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (lane == 0) c = __hip_atomic_fetch_add(&bq_claim, want, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             c = __builtin_amdgcn_readfirstlane(c);
             const uint32_t g = c >> 16, old = c & 0xffffu;
-            const uint32_t lo = __builtin_amdgcn_readfirstlane(bq_seg[g & 7][0]);
-            const uint32_t hi = __builtin_amdgcn_readfirstlane(bq_seg[g & 7][1]);
+            const uint32_t lo = __builtin_amdgcn_readfirstlane(bq_seg[g & 15][0]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane(bq_seg[g & 15][1]);
             if (old < hi - lo) {
                 next = lo + old; end = min(next + want, hi);
-                ckind = __builtin_amdgcn_readfirstlane(bq_seg[g & 7][2]);
+                ckind = __builtin_amdgcn_readfirstlane(bq_seg[g & 15][2]);
                 return;
             }
             if (__hip_atomic_load(&bq_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) { exhausted = true; return; }
@@ -821,7 +821,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     dequeue();
                 } while (!exhausted && next >= end);            // skip empty segments
                 if (lane == 0) {
-                    const uint32_t q = (g + 1) & 7;
+                    const uint32_t q = (g + 1) & 15;
                     bq_seg[q][0] = exhausted ? 0u : next;
                     bq_seg[q][1] = exhausted ? 0u : end;
                     bq_seg[q][2] = ckind;

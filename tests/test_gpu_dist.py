@@ -63,7 +63,8 @@ def test_rccl_gather_two_ranks_one_gpu(tmp_path):
     if r.returncode != 0:
         msg = r.stderr[-3000:]
         if "uplicate GPU" in msg or "invalid usage" in msg.lower():
-            pytest.skip("RCCL refuses two ranks on one GPU: " + msg.strip().splitlines()[-1][:200])
+            why = [ln for ln in msg.splitlines() if "uplicate GPU" in ln or "invalid usage" in ln.lower()]
+            pytest.skip("RCCL refuses two ranks on one GPU: " + (why[0].strip()[:200] if why else "duplicate device"))
         raise AssertionError(msg)
     x, y = _single_rank_c4(None), np.load(out)
     assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
