@@ -587,6 +587,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_BLOCKQ
 #define WF_BLOCKQ 1         // block-level ray queue shared by a block's waves (see the trace kernel)
 #endif
+#ifndef WF_BQ_PREFETCH
+#define WF_BQ_PREFETCH 0    // block queue: fetch the next segment when fewer rays than this remain (0 = off)
+#endif
 #ifndef WF_SUB
 #define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
 #endif
@@ -755,14 +758,14 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         // move on when it runs dry, so the global sweep order is unchanged
         // while each counter sees 1/WF_QSHARDS of the device-scope atomics
         uint32_t seg = nseg;
-        for (;;) {
+        while (qpart < WF_QSHARDS) {           // (qpart only grows: every shard it passed is dry)
             const uint32_t p = (blockIdx.x + qpart) % WF_QSHARDS;
             uint32_t t = 0;
             if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
             t = __builtin_amdgcn_readfirstlane(t);
             const uint32_t item = t * WF_QSHARDS + p;
             if (item < nseg) { seg = item; break; }
-            if (++qpart == WF_QSHARDS) break;
+            ++qpart;
         }
         if (seg >= nseg) { exhausted = true; if (WF_TIMING) { t_exh = __builtin_amdgcn_s_memrealtime(); witer_exh = witer; } }
         else {
@@ -788,13 +791,22 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     // up (a compare-and-swap on bq_refill) dequeues the next global segment and
     // publishes it as generation g + 1, the others sleep until then.  The last
     // segment of a block is thus worked through by all its waves, not by one.
-    __shared__ uint32_t bq_claim, bq_refill, bq_done;
-    __shared__ uint32_t bq_seg[16][3];
+    // WF_BQ_PREFETCH > 0: the wave whose claim leaves fewer rays than that fetches
+    // the block's next segment into bq_pf_seg (bq_pf: 0 empty, 1 being fetched,
+    // 2 ready), so the generation switch waits for no global atomic.
+    __shared__ uint32_t bq_claim, bq_refill, bq_done, bq_pf, bq_pf_done;
+    __shared__ uint32_t bq_seg[16][3], bq_pf_seg[3];
     if (threadIdx.x == 0) {
-        bq_claim = 0u; bq_refill = 0u; bq_done = 0u;
+        bq_claim = 0u; bq_refill = 0u; bq_done = 0u; bq_pf = 0u; bq_pf_done = 0u;
         bq_seg[0][0] = bq_seg[0][1] = 0u; bq_seg[0][2] = 0u;
     }
     __syncthreads();
+    // the next non-empty global segment into next / end / ckind, or exhausted
+    auto fetch_segment = [&]() {
+        do {
+            dequeue();
+        } while (!exhausted && next >= end);
+    };
     auto bclaim = [&](uint32_t want) {
         for (uint32_t guard = 0; guard < (1u << 10); ++guard) {
             uint32_t c = 0;
@@ -806,6 +818,26 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (old < hi - lo) {
                 next = lo + old; end = min(next + want, hi);
                 ckind = __builtin_amdgcn_readfirstlane(bq_seg[g & 15][2]);
+                if (WF_BQ_PREFETCH && old + want + WF_BQ_PREFETCH >= hi - lo) {
+                    uint32_t got = 0;
+                    if (lane == 0) {
+                        uint32_t e = 0;
+                        got = __hip_atomic_compare_exchange_strong(&bq_pf, &e, 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                                   __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+                    }
+                    if (__builtin_amdgcn_readfirstlane(got)) {   // fetch the block's next segment now
+                        const uint32_t sn = next, se = end, sk = ckind;
+                        fetch_segment();
+                        if (lane == 0) {
+                            bq_pf_seg[0] = exhausted ? 0u : next;
+                            bq_pf_seg[1] = exhausted ? 0u : end;
+                            bq_pf_seg[2] = ckind;
+                            bq_pf_done = exhausted ? 1u : 0u;
+                            __hip_atomic_store(&bq_pf, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        next = sn; end = se; ckind = sk; exhausted = false;
+                    }
+                }
                 return;
             }
             if (__hip_atomic_load(&bq_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) { exhausted = true; return; }
@@ -816,10 +848,25 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                                                            __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
             }
             won = __builtin_amdgcn_readfirstlane(won);
-            if (won) {                          // this wave fetches generation g + 1
-                do {
-                    dequeue();
-                } while (!exhausted && next >= end);            // skip empty segments
+            if (won) {                          // this wave publishes generation g + 1
+                uint32_t pf = 0;
+                if (WF_BQ_PREFETCH) {
+                    for (uint32_t w = 0; w < (1u << 16); ++w) {  // a prefetch in progress: wait for it
+                        pf = __hip_atomic_load(&bq_pf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (pf != 1u) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    pf = __builtin_amdgcn_readfirstlane(pf);
+                }
+                if (pf == 2u) {                 // the prefetched segment
+                    next = __builtin_amdgcn_readfirstlane(bq_pf_seg[0]);
+                    end = __builtin_amdgcn_readfirstlane(bq_pf_seg[1]);
+                    ckind = __builtin_amdgcn_readfirstlane(bq_pf_seg[2]);
+                    exhausted = __builtin_amdgcn_readfirstlane(bq_pf_done) != 0u;
+                    if (lane == 0) __hip_atomic_store(&bq_pf, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    fetch_segment();            // skips empty segments
+                }
                 if (lane == 0) {
                     const uint32_t q = (g + 1) & 15;
                     bq_seg[q][0] = exhausted ? 0u : next;

@@ -10,7 +10,7 @@ O=gpurun_out/vs; mkdir -p $O
 export TMPDIR=/tmp
 for v in ${CHECK}; do
   PNRT_DEVICE_LIB=$PWD/pnraytracing_amd/variants/libpnrt_$v.so timeout -k 10 300 python -u -m pytest -x -q \
-    --timeout 200 --timeout-method thread tests/test_gpu_fullsize.py tests/test_gpu_parity.py tests/test_gpu_fuzz.py \
+    --timeout ${CHECK_TIMEOUT:-200} --timeout-method thread tests/test_gpu_fullsize.py tests/test_gpu_parity.py tests/test_gpu_fuzz.py \
     ${PYTEST_K} > $O/check_$v.log 2>&1
   rc=$?; echo "check $v rc=$rc $(tail -1 $O/check_$v.log)"; [ $rc -eq 0 ] || exit $rc
 done
