@@ -78,6 +78,9 @@ def parse():
                          "--stats run whose trace-kernel average is the roofline's exclusive kernel_ms")
     ap.add_argument("--save-image", default="")
     ap.add_argument("--spp", type=int, default=0, help="experiment: samples per step other than the config's 4")
+    ap.add_argument("--iters-per-call", type=int, default=1,
+                    help="4-spp iterations per pnrt_render call (and per gather); steps stay 4-spp iterations "
+                         "(--steps / --warmup are rounded up to a multiple)")
     ap.add_argument("--kernel-times", action="store_true",
                     help="time every kernel class with HIP events in the timed region (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -147,6 +150,8 @@ def live_pmc(args):
                    "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
             if args.spp:
                 cmd += ["--spp", str(args.spp)]
+            if args.iters_per_call > 1:
+                cmd += ["--iters-per-call", str(args.iters_per_call)]
             log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
             t = time.perf_counter()
             with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
@@ -289,8 +294,14 @@ def main():
     sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
     image = None
 
+    ipc = max(1, args.iters_per_call)
+    args.steps = -(-args.steps // ipc) * ipc
+    args.warmup = -(-args.warmup // ipc) * ipc
+
     def step(k):
-        sf.render(spp * k, spp)
+        if k % ipc:                            # rendered by the call of its group's first iteration
+            return
+        sf.render(spp * k, spp * ipc)
         if world > 1:
             sf.gather_async()                  # one RCCL gather of the row bands to rank 0, overlapped
                                                # with the next step's rendering
@@ -432,6 +443,7 @@ def main():
             "data": "synthetic: procedural stand-in meshes (reference OBJs absent), reference HDR/texture assets",
             "config": {"workload": f"{cfg.name}: {cfg.description}", "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
+                       "iters_per_call": ipc,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
                        "kernel": kfull},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,

@@ -68,3 +68,16 @@ def test_rccl_gather_two_ranks_one_gpu(tmp_path):
         raise AssertionError(msg)
     x, y = _single_rank_c4(None), np.load(out)
     assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_bench_iters_per_call_same_image(tmp_path):
+    """bench.py --iters-per-call 2 renders two 4-spp iterations per pnrt_render
+    call (and per gather): the accumulated image equals one call per iteration."""
+    args = ["--steps", "2", "--warmup", "2", "--no-cpu-baseline", "--no-pmc", "--serial-steps", "0", "--config", "C4"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    a, b = str(tmp_path / "ipc1.npy"), str(tmp_path / "ipc2.npy")
+    for out, ipc in ((a, "1"), (b, "2")):
+        subprocess.run([sys.executable, "bench.py", *args, "--iters-per-call", ipc, "--save-image", out], cwd=REPO,
+                       env=env, check=True, timeout=400, stdout=subprocess.DEVNULL)
+    x, y = np.load(a), np.load(b)
+    assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
