@@ -45,7 +45,7 @@ def _parse_mtl(path: str) -> dict:
     if not os.path.exists(path):
         return out
     base = os.path.dirname(path)
-    with open(path, "r", errors="replace") as f:
+    with open(path, "r", encoding="utf-8", errors="replace") as f:      # Blender writes UTF-8 names
         for line in f:
             t = line.split()
             if not t or t[0].startswith("#"):
@@ -76,7 +76,7 @@ def load_obj(path: str) -> list[ObjMesh]:
     runs: list = []                # [object, material, faces (corner tuples)]
     obj_name, mat_name = "defaultobject", ""
     new_mesh = True
-    with open(path, "r", errors="replace") as f:
+    with open(path, "r", encoding="utf-8", errors="replace") as f:
         for line in f:
             t = line.split()
             if not t or t[0].startswith("#"):
@@ -166,3 +166,33 @@ def add_obj(builder, path: str, ops, material, name: str = "", textures: Texture
     textures = textures if textures is not None else TextureTable()
     tex_ids = [textures.id_for(m.diffuse_texture) for m in meshes]
     return builder.add_model([m.mesh for m in meshes], ops, material, name, texture_ids=tex_ids)
+
+
+def write_obj(path: str, meshes, material_names=None, mtllib: str | None = None) -> None:
+    """Write meshes as a Wavefront OBJ that :func:`load_obj` reads back to the
+    same triangles: one ``o``/``usemtl`` per mesh, positions and normals as
+    ``%.9g`` (float32 round-trips exactly), texcoords stored pre-flipped
+    (``vt u 1-v``) for FlipUVs, faces in index order.  (Scene export for tests
+    and tools; the reference only reads OBJ.)"""
+    with open(path, "w", encoding="utf-8") as f:
+        if mtllib:
+            f.write(f"mtllib {mtllib}\n")
+        base = 0
+        for k, m in enumerate(meshes):
+            f.write(f"o mesh{k}\n")
+            if material_names:
+                f.write(f"usemtl {material_names[k]}\n")
+            P = np.asarray(m.positions, np.float32)
+            Nn = np.asarray(m.normals, np.float32) if m.normals is not None else np.zeros_like(P)
+            T = np.asarray(m.texcoords, np.float32) if m.texcoords is not None else np.zeros((len(P), 2), np.float32)
+            for p in P:
+                f.write("v %.9g %.9g %.9g\n" % tuple(float(x) for x in p))
+            for t in T:
+                f.write("vt %.9g %.9g\n" % (float(t[0]), float(np.float32(1.0) - t[1])))
+            for n in Nn:
+                f.write("vn %.9g %.9g %.9g\n" % tuple(float(x) for x in n))
+            idx = np.asarray(m.indices, np.int64).reshape(-1, 3) + base + 1
+            for a, b, c in idx:
+                f.write(f"f {a}/{a}/{a} {b}/{b}/{b} {c}/{c}/{c}\n")
+            base += len(P)
+

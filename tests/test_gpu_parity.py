@@ -254,3 +254,17 @@ def test_errors_are_reported(pt):
     with pytest.raises(PnrtError):
         t.upload_scene(dataclasses.replace(c.packed, triangles=bad))
     t.close()
+
+
+def test_obj_ingested_scene_bitwise(pt, tmp_path):
+    """SURVEY 8f row 1 on the GPU: C4's meshes written as OBJ files and read back
+    through pnraytracing_amd.obj (unshared per-corner vertices, as Assimp
+    builds them) render the same image as the procedural scene, and the oracle's."""
+    import dataclasses
+    import test_obj
+    base = cfg("C4", width=192, height=108)
+    c = dataclasses.replace(base, name="C4-obj", packed=test_obj._teapot_scene(str(tmp_path)))
+    got = gpu_render(pt, c, 0, 4)
+    ref, _ = pyoracle.Oracle(c).render(0, 4)
+    assert_bitwise(got, ref, "C4 via OBJ")
+    assert np.array_equal(got.view(np.uint32), gpu_render(pt, base, 0, 4).view(np.uint32))

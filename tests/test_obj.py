@@ -3,6 +3,8 @@ row 1).  Assimp itself is absent, so parity is pinned only by these
 hand-built files: unshared per-corner vertices, fan triangulation (concave
 quads fan from the concave corner), FlipUVs, negative indices, mesh splits at
 o/g/usemtl, map_Kd texture dedup."""
+import os
+
 import numpy as np
 
 from pnraytracing_amd import host as H
@@ -74,3 +76,61 @@ def test_add_obj_texture_ids(tmp_path):
     tex = p.triangles[:, 4].astype(int)
     assert sorted(set(tex.tolist())) == [-1, 0]
     assert len(p.triangles) == 2 * (2 + 1 + 3)
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_reference_mtl_files():
+    """The reference's own MTL files (model/marry/Marry.mtl, model/floor/floor.mtl,
+    committed under tests/golden as data): Blender's UTF-8 material names and
+    map_Kd resolved next to the MTL file (model.hpp:57-77 loads it from there)."""
+    m = obj._parse_mtl(os.path.join(GOLDEN, "Marry.mtl"))
+    assert list(m) == ["MC003_Kozakura_Mari", "材质"]
+    assert m["MC003_Kozakura_Mari"] == os.path.join(GOLDEN, "MC003_Kozakura_Mari.png") and m["材质"] is None
+    assert obj._parse_mtl(os.path.join(GOLDEN, "floor.mtl")) == {"None": None}
+
+
+def test_usemtl_utf8_names_split_meshes(tmp_path):
+    import shutil
+    shutil.copy(os.path.join(GOLDEN, "Marry.mtl"), tmp_path / "Marry.mtl")
+    text = ("mtllib Marry.mtl\nv 0 0 0\nv 1 0 0\nv 0 1 0\nv 1 1 0\no Mari\nusemtl MC003_Kozakura_Mari\n"
+            "f 1 2 3\nusemtl 材质\nf 2 4 3\nusemtl 材质\nf 1 2 4\n")
+    (tmp_path / "m.obj").write_text(text, encoding="utf-8")
+    ms = obj.load_obj(str(tmp_path / "m.obj"))
+    assert [(x.material_name, len(x.mesh.indices) // 3) for x in ms] == [("MC003_Kozakura_Mari", 1), ("材质", 2)]
+    assert ms[0].diffuse_texture == str(tmp_path / "MC003_Kozakura_Mari.png") and ms[1].diffuse_texture is None
+
+
+def _teapot_scene(via_obj_dir=None):
+    """C4's geometry (teapot + floor + area light), its meshes either built
+    procedurally or written to OBJ files and loaded back through load_obj."""
+    sb = H.SceneBuilder()
+    meshes = [H.mesh_teapot(), H.mesh_quad(27.5), H.mesh_quad(27.5)]
+    if via_obj_dir is not None:
+        for k, m in enumerate(meshes):
+            p = os.path.join(via_obj_dir, f"m{k}.obj")
+            obj.write_obj(p, [m])
+            meshes[k] = [x.mesh for x in obj.load_obj(p)]
+    sb.add_model(meshes[0], [H.scale(0.2)], H.Material(baseColor=(0.6, 0.7, 0.2), metallic=0.7, roughness=0.3), "teapot")
+    sb.add_model(meshes[1], [H.scale(1.0)], H.Material(baseColor=(0.73, 0.73, 0.73), metallic=0.2, roughness=0.85),
+                 "floor")
+    sb.add_model(meshes[2], [H.translate(1.5, 3.0, 1.0), H.rotate(180.0, 0, 0, 1), H.scale(0.02)],
+                 H.Material(baseColor=(0.73, 0.73, 0.73), emssive=(8.0, 8.0, 8.0)), "area_light")
+    return sb.build()
+
+
+def test_obj_round_trip_same_triangles_and_bvh(tmp_path):
+    """Meshes written as OBJ and read back (unshared per-corner vertices, as
+    Assimp builds them) give the same triangles, BVH, light list and materials
+    as the procedural meshes; only the vertex array is unshared."""
+    a, b = _teapot_scene(), _teapot_scene(str(tmp_path))
+    for name in ("nodes", "lights", "materials"):
+        x, y = getattr(a, name), getattr(b, name)
+        assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32)), name
+    ta, tb = a.triangles.reshape(-1, 6), b.triangles.reshape(-1, 6)
+    va, vb = a.vertices.reshape(-1, 15), b.vertices.reshape(-1, 15)
+    assert len(ta) == len(tb) and len(vb) == 3 * len(tb)
+    for k in range(3):       # corner k of every triangle: same position and normal (cols 0-5)
+        pa, pb = va[ta[:, k].astype(np.int64), :6], vb[tb[:, k].astype(np.int64), :6]
+        assert np.array_equal(pa.view(np.uint32), pb.view(np.uint32))
