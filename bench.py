@@ -78,9 +78,11 @@ def parse():
                          "--stats run whose trace-kernel average is the roofline's exclusive kernel_ms")
     ap.add_argument("--save-image", default="")
     ap.add_argument("--spp", type=int, default=0, help="experiment: samples per step other than the config's 4")
-    ap.add_argument("--iters-per-call", type=int, default=1,
-                    help="4-spp iterations per pnrt_render call (and per gather); steps stay 4-spp iterations "
-                         "(--steps / --warmup are rounded up to a multiple)")
+    ap.add_argument("--iters-per-call", type=int, default=2,
+                    help="4-spp iterations per pnrt_render call and per gather of the accumulated rows "
+                         "(the primary pass and each launch's drain amortised over them; the image is the "
+                         "same); steps stay 4-spp iterations, the last call of the warm-up / the timed "
+                         "region takes what is left")
     ap.add_argument("--kernel-times", action="store_true",
                     help="time every kernel class with HIP events in the timed region (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -139,7 +141,8 @@ def live_pmc(args):
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(v, None)
-    steps, warm = 2, 1
+    ipc = max(1, args.iters_per_call)
+    steps, warm = 2 * ipc, ipc           # whole calls only: every launch covers ipc iterations
     counters = {}
     try:
         for i, group in enumerate(PMC_PASSES):
@@ -150,8 +153,7 @@ def live_pmc(args):
                    "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
             if args.spp:
                 cmd += ["--spp", str(args.spp)]
-            if args.iters_per_call > 1:
-                cmd += ["--iters-per-call", str(args.iters_per_call)]
+            cmd += ["--iters-per-call", str(args.iters_per_call)]
             log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
             t = time.perf_counter()
             with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
@@ -295,19 +297,20 @@ def main():
     image = None
 
     ipc = max(1, args.iters_per_call)
-    args.steps = -(-args.steps // ipc) * ipc
-    args.warmup = -(-args.warmup // ipc) * ipc
 
-    def step(k):
-        if k % ipc:                            # rendered by the call of its group's first iteration
+    def step(k, lo=0, hi=1 << 30):
+        """Iteration k of [lo, hi): the call of its group (ipc iterations from lo,
+        the group cut at hi) is issued at the group's first iteration."""
+        if (k - lo) % ipc:
             return
-        sf.render(spp * k, spp * ipc)
+        n = min(ipc, hi - k)
+        sf.render(spp * k, spp * n)
         if world > 1:
             sf.gather_async()                  # one RCCL gather of the row bands to rank 0, overlapped
                                                # with the next step's rendering
 
     for k in range(args.warmup):
-        step(k)
+        step(k, 0, args.warmup)
     if world > 1:
         sf.finish()
     torch.cuda.synchronize()
@@ -316,7 +319,7 @@ def main():
     torch.cuda.synchronize()
     if args.child:                             # a PMC pass: the profiler sees the launches; done
         for k in range(args.steps):
-            step(args.warmup + k)
+            step(args.warmup + k, args.warmup, args.warmup + args.steps)
         torch.cuda.synchronize()
         pt.close()
         return
@@ -329,7 +332,7 @@ def main():
     pt.profile_enable(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k)
+        step(args.warmup + k, args.warmup, args.warmup + args.steps)
     if world > 1:
         image = sf.finish()                    # every gather completes inside the timed region
     torch.cuda.synchronize()
@@ -353,13 +356,13 @@ def main():
         pt.set_options(opts | SERIAL)
         pt.profile_select(None)
         pt.profile_enable(True)
-        for k in range(args.serial_steps):
-            sf.render(spp * (args.warmup + args.steps + k), spp)
+        for k in range(args.serial_steps):          # calls of the same size as the timed ones
+            sf.render(spp * (args.warmup + args.steps + k * ipc), spp * ipc)
         torch.cuda.synchronize()
         ser = pt.profile_read()
         pt.profile_enable(False)
         pt.set_options(opts)
-        excl = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / args.serial_steps}
+        excl = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / (args.serial_steps * ipc)}
                 for k, (ms, n) in ser.items() if n}
     kern_ms = excl[kname]["ms_per_launch"] if kname in excl else None
     if world > 1:
@@ -422,7 +425,8 @@ def main():
         census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
         requested = None
         if census and kern_ms:
-            rb = census["requested_bytes_per_launch"] * rows0 / census.get("rows", H)
+            rb = (census["requested_bytes_per_launch"] * rows0 / census.get("rows", H)
+                  * spp * ipc / census.get("frames", 4))        # the census traced 4-frame calls
             requested = {"bytes_per_launch": round(rb), "achieved": round(rb / (kern_ms * 1e-3) / 1e9, 1),
                          "peak": L2_PEAK_GBS, "unit": "GB/s",
                          "frac_of_l2": round(rb / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),

@@ -184,8 +184,10 @@ static int prof_collect(pnrt_ctx* c) {
 
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
-    (void)sync_all(c);
-    (void)hipFree(*p);
+    if (*p) {                          // the old buffer may still be in use by calls in flight
+        (void)sync_all(c);
+        (void)hipFree(*p);
+    }
     *p = nullptr;
     *cap = 0;
     HIPCHK(c, hipMalloc(p, bytes));
@@ -409,12 +411,17 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     const size_t ovf_bytes = (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8;
     const uint32_t cfA0 = split ? (chunk + 1) / 2 : chunk;
     const size_t bytesA = wf_bytes(per_frame * cfA0), bytesB = split ? wf_bytes(per_frame * (chunk - cfA0)) : 0;
-    if ((rc = grow(c, (void**)&P.primary, &P.primary_cap, pix * 48)) ||
-        (rc = grow(c, (void**)&P.colors, &P.colors_cap, pix * 16 * chunk)) ||
-        (rc = grow(c, &P.wf, &P.wf_cap, bytesA + bytesB + 512)) ||
-        (rc = grow(c, (void**)&P.ovf[0], &P.ovf_cap[0], ovf_bytes)) ||
-        (split && (rc = grow(c, (void**)&P.ovf[1], &P.ovf_cap[1], ovf_bytes))))
-        return rc;
+    // every buffer set this call size rotates over is sized now, so no later call of
+    // the same size reallocates (a reallocation waits for all calls in flight)
+    for (unsigned q = 0; q < npipes; ++q) {
+        pnrt_ctx::Pipe& Q = c->pipe[(pi + q) % npipes];
+        if ((rc = grow(c, (void**)&Q.primary, &Q.primary_cap, pix * 48)) ||
+            (rc = grow(c, (void**)&Q.colors, &Q.colors_cap, pix * 16 * chunk)) ||
+            (rc = grow(c, &Q.wf, &Q.wf_cap, bytesA + bytesB + 512)) ||
+            (rc = grow(c, (void**)&Q.ovf[0], &Q.ovf_cap[0], ovf_bytes)) ||
+            (split && (rc = grow(c, (void**)&Q.ovf[1], &Q.ovf_cap[1], ovf_bytes))))
+            return rc;
+    }
     ++c->ncall;
     hipStream_t w0 = P.w[0], w1 = P.w[1] ? P.w[1] : P.w[0];
     // this pipe's buffers were last read by the blend of the call that used it last

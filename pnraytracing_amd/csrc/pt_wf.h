@@ -42,10 +42,10 @@
 #define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
 #endif
 #ifndef WF_TRACE_BLOCK
-#define WF_TRACE_BLOCK 256   // trace workgroup size (128 or 256)
+#define WF_TRACE_BLOCK 256   // trace workgroup size (128, 256 or 512)
 #endif
 #define WF_SPA_STRIDE (WF_TRACE_BLOCK * 8u)                 // LDS bytes per stack depth
-#define WF_SPA_SHIFT (WF_TRACE_BLOCK == 256 ? 11 : 10)
+#define WF_SPA_SHIFT (WF_TRACE_BLOCK == 512 ? 12 : WF_TRACE_BLOCK == 256 ? 11 : 10)
 #define WF_CHUNK 256u        // rays per dequeue
 #ifndef WF_CONT_FROM_STATE
 #define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued

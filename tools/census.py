@@ -58,7 +58,7 @@ def main(names):
         node = sum(x[4] for x in b)
         rays = sum(x[7] for x in b)
         req = 64 * node + 48 * tri + 36 * rays
-        res[cname] = {"source_hash": build.device_source_hash(), "rows": rows, "trace_launches": launches,
+        res[cname] = {"source_hash": build.device_source_hash(), "rows": rows, "frames": 4, "trace_launches": launches,
                       "per_bounce": [{"bounce": x[0], "paths": x[1], "iters": x[2], "tri_steps": x[3],
                                       "node_steps": x[4], "rays": x[7]} for x in b],
                       "lane_steps_per_ray": round((tri + node) / max(rays, 1), 3),

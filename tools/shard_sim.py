@@ -19,12 +19,12 @@ with PathTracer(0) as pt:
     pt.load(cfg)
     for n in (1, 2, 4, 8):
         rows = len(shard_rows(cfg.height, 8, n, 0))
-        for k in range(3):
+        for k in range(4):                  # every buffer set allocated before timing
             pt.render(fpc * k, fpc, 8, n, 0)
         pt.synchronize()
         t = time.perf_counter()
         for k in range(steps):
-            pt.render(fpc * (3 + k), fpc, 8, n, 0)
+            pt.render(fpc * (4 + k), fpc, 8, n, 0)
         pt.synchronize()
         dt = (time.perf_counter() - t) / steps
         per_rank = rows * cfg.width * fpc / dt / 1e6
