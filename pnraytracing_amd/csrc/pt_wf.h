@@ -28,7 +28,7 @@
 #define WF_PIPES_LARGE (WF_PIPES > 3 ? 3 : WF_PIPES)   // calls in flight for large calls (+ the context
 #endif                                                // stream = the 4 HW queues of a process)
 #ifndef WF_SMALL_CALL_PATHS
-#define WF_SMALL_CALL_PATHS 1500000   // calls with fewer paths (multi-GPU shares) use all WF_PIPES sets
+#define WF_SMALL_CALL_PATHS 5000000   // calls with fewer paths (multi-GPU shares: 2.1M at N = 8, 4.2M at N = 4 with 8-frame calls) use all WF_PIPES sets
 #endif
 #ifndef WF_SPLIT
 #define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
