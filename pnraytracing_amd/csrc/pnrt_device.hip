@@ -394,8 +394,14 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     if (per_frame > (size_t)WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: frame too large for one batch");
     const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
     const uint32_t chunk = nf < fit ? nf : fit;
+    // calls in flight by call size: small (multi-GPU shares) 4 with > 4 hardware queues;
+    // 1080p-class calls 2 -- their launches are long enough to fill each other's
+    // drains (C2 +1.8 %, C3 +2.7 %, C4 +1.6 % against 3); 4K-class calls 3, which
+    // hide more of their HBM-latency-bound traversal (C5 -3.5 % with 2)
+    const size_t call_paths = per_frame * chunk;
     const unsigned npipes = c->serial ? 1u
-                          : per_frame * chunk < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small : WF_PIPES_LARGE;
+                          : call_paths < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small
+                          : call_paths < (size_t)WF_HUGE_CALL_PATHS ? WF_PIPES_MEDIUM : WF_PIPES_LARGE;
     const unsigned pi = c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;
     pnrt_ctx::Pipe& P = c->pipe[pi];

@@ -27,6 +27,12 @@
 #ifndef WF_PIPES_LARGE
 #define WF_PIPES_LARGE (WF_PIPES > 3 ? 3 : WF_PIPES)   // calls in flight for large calls (+ the context
 #endif                                                // stream = the 4 HW queues of a process)
+#ifndef WF_PIPES_MEDIUM
+#define WF_PIPES_MEDIUM 2   // calls in flight for calls of WF_SMALL_CALL_PATHS .. WF_HUGE_CALL_PATHS paths
+#endif
+#ifndef WF_HUGE_CALL_PATHS
+#define WF_HUGE_CALL_PATHS 32000000   // calls with more paths (4K frames) keep WF_PIPES_LARGE in flight
+#endif
 #ifndef WF_SMALL_CALL_PATHS
 #define WF_SMALL_CALL_PATHS 5000000   // calls with fewer paths (multi-GPU shares: 2.1M at N = 8, 4.2M at N = 4 with 8-frame calls) use all WF_PIPES sets
 #endif
