@@ -399,9 +399,10 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     // drains (C2 +1.8 %, C3 +2.7 %, C4 +1.6 % against 3); 4K-class calls 3, which
     // hide more of their HBM-latency-bound traversal (C5 -3.5 % with 2)
     const size_t call_paths = per_frame * chunk;
-    const unsigned npipes = c->serial ? 1u
-                          : call_paths < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small
-                          : call_paths < (size_t)WF_HUGE_CALL_PATHS ? WF_PIPES_MEDIUM : WF_PIPES_LARGE;
+    const unsigned want = c->serial ? 1u
+                        : call_paths < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small
+                        : call_paths < (size_t)WF_HUGE_CALL_PATHS ? WF_PIPES_MEDIUM : WF_PIPES_LARGE;
+    const unsigned npipes = std::max(1u, std::min(want, c->n_pipes_small));   // only sets pipes_init made
     const unsigned pi = c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;
     pnrt_ctx::Pipe& P = c->pipe[pi];

@@ -28,8 +28,8 @@
 #define WF_PIPES_LARGE (WF_PIPES > 3 ? 3 : WF_PIPES)   // calls in flight for large calls (+ the context
 #endif                                                // stream = the 4 HW queues of a process)
 #ifndef WF_PIPES_MEDIUM
-#define WF_PIPES_MEDIUM 2   // calls in flight for calls of WF_SMALL_CALL_PATHS .. WF_HUGE_CALL_PATHS paths
-#endif
+#define WF_PIPES_MEDIUM (WF_PIPES > 2 ? 2 : WF_PIPES)   // calls in flight for calls of WF_SMALL_CALL_PATHS ..
+#endif                                                  // WF_HUGE_CALL_PATHS paths (never more than the sets made)
 #ifndef WF_HUGE_CALL_PATHS
 #define WF_HUGE_CALL_PATHS 32000000   // calls with more paths (4K frames) keep WF_PIPES_LARGE in flight
 #endif
