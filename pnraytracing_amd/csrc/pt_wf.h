@@ -610,106 +610,6 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
-// ---- cooperative record fetch (WF_COOPLOAD, measured slower: off) ---------------------------
-// A step reads one 64-B record per lane with four 16-B loads.  Issued per lane
-// (mode 0, kept) every load instruction touches one cache line per lane.  In a
-// dependent-gather microbenchmark of this shape (tools/microtests/gather_test.hip)
-// the per-lane form runs at the same rate with 0 or 120 VALU per step -- the
-// vector L1's per-line lookups bound it -- and sharing each instruction's
-// lines between lanes doubles the load-side rate.  Cooperative fetches:
-//   mode 1 (quad): in instruction k the four lanes of a quad read the four
-//     quarters of the record of quad lane k (one line per quad per instruction,
-//     4x fewer lookups), then a 4x4 in-quad transpose (two butterfly stages);
-//   mode 2 (pair): in instructions k = 0, 1 the two lanes of a pair read
-//     quarters (2k, 2k + 1) of the even lane's record, in k = 2, 3 of the odd
-//     lane's (2x fewer lookups), then one butterfly stage.
-// Both are bit-exact and slower in the trace kernel (exclusive launch 1.58 ->
-// 1.97 ms quad, 1.79 ms pair): its lanes already share lines (36 per load
-// instruction, L1 hit 93 %), and the exchange's 16-32 VALU, the wait for all
-// four quarters and the address broadcast land on the step's critical path.
-// A butterfly stage is v_cndmask with a DPP operand, executed by every lane of
-// the wave (a DPP read of a lane the compiler had predicated off returns 0).
-#ifndef WF_COOPLOAD
-#define WF_COOPLOAD 0
-#endif
-#ifndef WF_POP_EARLY
-#define WF_POP_EARLY 0
-#endif
-#define WF_QP(a, b, c, d) ((a) | ((b) << 2) | ((c) << 4) | ((d) << 6))
-// o0 = lane in m02 ? i0 : partner's i1;  o2 = lane in m02 ? i2 : partner's i3
-// o1 = lane in m13 ? i1 : partner's i0;  o3 = lane in m13 ? i3 : partner's i2
-// (partner = the quad lane PERM names).  s_nop 1 covers the VALU-write ->
-// DPP-read hazard on results of a previous stage.
-#define WF_BUTTERFLY(NAME, PERM)                                                                              \
-    PN_DEV void NAME(uint32_t i0, uint32_t i1, uint32_t i2, uint32_t i3, uint64_t m02, uint64_t m13, uint32_t& o0, \
-                     uint32_t& o1, uint32_t& o2, uint32_t& o3) {                                                 \
-        asm("s_mov_b64 vcc, %8\n\ts_nop 1\n\t"                                                                   \
-            "v_cndmask_b32_dpp %0, %5, %4, vcc quad_perm:" PERM " row_mask:0xf bank_mask:0xf\n\t"                \
-            "v_cndmask_b32_dpp %2, %7, %6, vcc quad_perm:" PERM " row_mask:0xf bank_mask:0xf\n\t"                \
-            "s_mov_b64 vcc, %9\n\t"                                                                              \
-            "v_cndmask_b32_dpp %1, %4, %5, vcc quad_perm:" PERM " row_mask:0xf bank_mask:0xf\n\t"                \
-            "v_cndmask_b32_dpp %3, %6, %7, vcc quad_perm:" PERM " row_mask:0xf bank_mask:0xf"                     \
-            : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3)                                                         \
-            : "v"(i0), "v"(i1), "v"(i2), "v"(i3), "s"(m02), "s"(m13)                                             \
-            : "vcc");                                                                                             \
-    }
-WF_BUTTERFLY(wf_bfly_x1, "[1,0,3,2]")
-WF_BUTTERFLY(wf_bfly_x2, "[2,3,0,1]")
-#define WF_M_EVEN 0x5555555555555555ull
-#define WF_M_ODD 0xAAAAAAAAAAAAAAAAull
-#define WF_M_LO2 0x3333333333333333ull
-#define WF_M_HI2 0xCCCCCCCCCCCCCCCCull
-template <int PERM>
-PN_DEV uint32_t wf_qbcast(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, PERM, 0xf, 0xf, true);
-}
-typedef unsigned int wf_u4 __attribute__((ext_vector_type(4)));
-PN_DEV wf_u4 geo_load4(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-}
-PN_DEV float4 wf_f4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
-    return make_float4(__uint_as_float(x), __uint_as_float(y), __uint_as_float(z), __uint_as_float(w));
-}
-// The 64 B at byte offset `off` of this lane, fetched cooperatively.  Every lane
-// of the wave must call it (lanes without a record pass off = 0: node 0).
-PN_DEV void wf_coop_fetch(__amdgpu_buffer_rsrc_t geo, uint32_t off, float4& q0, float4& q1, float4& q2, float4& q3) {
-    const uint32_t c = __lane_id() & 3u;
-    if constexpr (WF_COOPLOAD == 1) {
-        const wf_u4 a0 = geo_load4(geo, wf_qbcast<WF_QP(0, 0, 0, 0)>(off) + 16u * c);
-        const wf_u4 a1 = geo_load4(geo, wf_qbcast<WF_QP(1, 1, 1, 1)>(off) + 16u * c);
-        const wf_u4 a2 = geo_load4(geo, wf_qbcast<WF_QP(2, 2, 2, 2)>(off) + 16u * c);
-        const wf_u4 a3 = geo_load4(geo, wf_qbcast<WF_QP(3, 3, 3, 3)>(off) + 16u * c);
-        // a_k = quarter c of quad lane k's record; B1[l][b] = ((l^b)&1) ? A[l^1][b^1] : A[l][b],
-        // then B2[l][b] = ((l^b)&2) ? B1[l^2][b^2] : B1[l][b] = quarter b of lane l's record
-        uint32_t b[4][4], w[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            wf_bfly_x1(a0[j], a1[j], a2[j], a3[j], WF_M_EVEN, WF_M_ODD, b[0][j], b[1][j], b[2][j], b[3][j]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            wf_bfly_x2(b[0][j], b[2][j], b[1][j], b[3][j], WF_M_LO2, WF_M_HI2, w[0][j], w[2][j], w[1][j], w[3][j]);
-        q0 = wf_f4(w[0][0], w[0][1], w[0][2], w[0][3]);
-        q1 = wf_f4(w[1][0], w[1][1], w[1][2], w[1][3]);
-        q2 = wf_f4(w[2][0], w[2][1], w[2][2], w[2][3]);
-        q3 = wf_f4(w[3][0], w[3][1], w[3][2], w[3][3]);
-    } else {
-        const uint32_t e = 16u * (c & 1u);
-        const uint32_t o0 = wf_qbcast<WF_QP(0, 0, 2, 2)>(off), o1 = wf_qbcast<WF_QP(1, 1, 3, 3)>(off);
-        const wf_u4 a0 = geo_load4(geo, o0 + e), a1 = geo_load4(geo, o0 + 32u + e);
-        const wf_u4 a2 = geo_load4(geo, o1 + e), a3 = geo_load4(geo, o1 + 32u + e);
-        // even lane: quarters (own a0, partner a0, own a1, partner a1) of its record;
-        // odd lane: (partner a2, own a2, partner a3, own a3)
-        uint32_t w[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            wf_bfly_x1(a0[j], a2[j], a1[j], a3[j], WF_M_EVEN, WF_M_ODD, w[0][j], w[1][j], w[2][j], w[3][j]);
-        q0 = wf_f4(w[0][0], w[0][1], w[0][2], w[0][3]);
-        q1 = wf_f4(w[1][0], w[1][1], w[1][2], w[1][3]);
-        q2 = wf_f4(w[2][0], w[2][1], w[2][2], w[2][3]);
-        q3 = wf_f4(w[3][0], w[3][1], w[3][2], w[3][3]);
-    }
-}
-
 // One lane's traversal state (a ray being traced).
 struct TravState {
     RayP r;
@@ -724,7 +624,7 @@ struct TravState {
 // (an any-hit ray accepted a triangle, or nothing is left to visit).
 template <int STK, bool ID>
 PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo,
-                                                   uint2* lds, TravState& t, float4 q0, float4 q1, float4 q2, float4 q3) {
+                                                   uint2* lds, TravState& t) {
     // One step, written branch-light: the triangle test and the node
     // visit are both evaluated (a wave almost always holds lanes of
     // both kinds, so both paths ran anyway) and their results are
@@ -732,27 +632,14 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // the result store) and the rare IEEE division stay in branches.
     const bool isTri = t.lc > 0;
     const bool isNode = !isTri & (t.cur != REF_NONE);
-    // WF_POP_EARLY (off: -1.5 to -2 %, bit-exact): the LDS stack top is read now,
-    // beside the record fetch, so a pop at the end of the step does not wait for
-    // the LDS round trip (a push in this step is what a pop would return: taken
-    // from registers)
-    uint2 pre = make_uint2(0u, 0u);
-    if constexpr (WF_POP_EARLY) {
-        const bool inLds = (t.spa >= WF_SPA_STRIDE) & (t.spa <= STK * WF_SPA_STRIDE);
-        const uint32_t pa = inLds ? t.spa - WF_SPA_STRIDE : (t.spa & (WF_SPA_STRIDE - 1u));
-        pre = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + pa);
-        asm volatile("" ::: "memory");     // issued ahead of the record fetch (the scheduler sinks it)
-    }
-    if constexpr (!WF_COOPLOAD) {
-        // ---- the step's single fetch: a triangle record or a node (lanes
-        // with neither re-read node 0, which stays in L1)
-        const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)t.lt * 48u : (isNode ? t.cur : 0u) * 64u;
-        // triangle lanes read the unused fourth quarter from one shared address
-        // (one cache access per wave instead of one per lane)
-        const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
-        q0 = geo_load(geo, off); q1 = geo_load(geo, off + 16u); q2 = geo_load(geo, off + 32u);
-        q3 = geo_load(geo, off3);
-    }
+    // ---- the step's single fetch: a triangle record or a node (lanes
+    // with neither re-read node 0, which stays in L1)
+    const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)t.lt * 48u : (isNode ? t.cur : 0u) * 64u;
+    // triangle lanes read the unused fourth quarter from one shared address
+    // (one cache access per wave instead of one per lane)
+    const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
+    const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
+                 q3 = geo_load(geo, off3);
     // triangle test (:254-357 / :360-424)
     float e0, e1, e2, det, ts;
     const bool acc = tri_test<ID>(t.r, q0, q1, q2, t.tMax, e0, e1, e2, det, ts) & isTri;
@@ -775,8 +662,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
     const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
     const float zFar = rightFirst ? zloL : zloR;
-    const bool pushed = hNear & hFar;
-    if (pushed) wf_push<STK>(lds, b, t.spa, farRef, zFar);
+    if (hNear & hFar) wf_push<STK>(lds, b, t.spa, farRef, zFar);
     const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
     int gs, gc;
@@ -788,14 +674,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool idle = !done & (t.lc <= 0) & (t.cur == REF_NONE);
     done = done | (idle & (t.spa < WF_SPA_STRIDE));
     if (idle & (t.spa >= WF_SPA_STRIDE)) {
-        uint2 e;
-        if constexpr (WF_POP_EARLY) {
-            if (pushed) { t.spa -= WF_SPA_STRIDE; e = make_uint2(farRef, __float_as_uint(zFar)); }
-            else if (t.spa <= STK * WF_SPA_STRIDE) { t.spa -= WF_SPA_STRIDE; e = pre; }
-            else e = wf_pop<STK>(lds, b, t.spa);
-        } else {
-            e = wf_pop<STK>(lds, b, t.spa);
-        }
+        const uint2 e = wf_pop<STK>(lds, b, t.spa);
         const float z = __uint_as_float(e.y);
         const bool culled = cull & (z > t.tMax * 1.000001f) & (z > 1e-20f);
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
@@ -1033,18 +912,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
         }
         if (WF_TIMING) ++witer;
-        float4 q0, q1, q2, q3;
-        if constexpr (WF_COOPLOAD != 0) {
-            // the step's record, fetched by the whole wave (idle lanes read node 0): a
-            // pending triangle (48 B; its fourth quarter, the next record's first, is
-            // unused -- the array has a 16-B tail pad) or the current node (64 B)
-            const bool isTri = t.lc > 0;
-            const bool isNode = !isTri & (t.cur != REF_NONE);
-            const uint32_t off = busy ? (isTri ? s.geo_tri_off + (uint32_t)t.lt * 48u : (isNode ? t.cur : 0u) * 64u) : 0u;
-            wf_coop_fetch(geo, off, q0, q1, q2, q3);
-        }
         if (busy) {
-            const bool done = wf_step<STK, ID>(s, b, geo, lds, t, q0, q1, q2, q3);
+            const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
             if (WF_STATS || WF_TIMING) t.nst += 1;
             if (WF_STATS && done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (rid >> 30) << 16 | min(t.nst, 0xffffu);

@@ -83,6 +83,7 @@ __global__ void __launch_bounds__(256, 8) gather_kernel(const uint32_t* table, u
         __builtin_amdgcn_make_buffer_rsrc((void*)table, (short)0, (int)(nrec * 64u), 0x00020000);
     const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63u, c = lane & 3u;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[MODE == 3 ? 4 * 1024 : 4];
     uint32_t r = (gid * 2654435761u) % nrec;
     uint32_t acc = 0;
     float f = (float)(gid & 7);
@@ -95,6 +96,31 @@ __global__ void __launch_bounds__(256, 8) gather_kernel(const uint32_t* table, u
             w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
             w[8] = cc.x; w[9] = cc.y; w[10] = cc.z; w[11] = cc.w;
             w[12] = d.x; w[13] = d.y; w[14] = d.z; w[15] = d.w;
+        } else if constexpr (MODE == 3) {
+            // quad fetch through LDS: in instruction k the lanes of quad q DMA the four
+            // quarters of quad lane k's record into this wave's 4-KB stage (lane L of
+            // instruction k lands at k * 1 KB + 16 L: lane 4q + c carries quarter
+            // (c - k) & 3, so the reads below are bank-conflict free); then every lane
+            // reads its own 64 B with four ds_read_b128
+            uint32_t* st = stage + (threadIdx.x >> 6) * 1024u;
+            const uint32_t kk = c;   // this lane is quad lane k = c for its own record
+            const uint32_t o0 = qp<QP(0, 0, 0, 0)>(r) * 64u, o1 = qp<QP(1, 1, 1, 1)>(r) * 64u,
+                           o2 = qp<QP(2, 2, 2, 2)>(r) * 64u, o3 = qp<QP(3, 3, 3, 3)>(r) * 64u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(st + 0 * 256), 16,
+                                                     o0 + 16u * ((c - 0u) & 3u), 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(st + 1 * 256), 16,
+                                                     o1 + 16u * ((c - 1u) & 3u), 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(st + 2 * 256), 16,
+                                                     o2 + 16u * ((c - 2u) & 3u), 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(st + 3 * 256), 16,
+                                                     o3 + 16u * ((c - 3u) & 3u), 0, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t q4 = (lane >> 2) * 4u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u4 v = *reinterpret_cast<const u4*>(st + kk * 256u + (q4 + ((j + kk) & 3u)) * 4u);
+                w[4 * j + 0] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+            }
         } else if constexpr (MODE == 2) {   // quad loads, no transpose (load side only; wrong words)
             const uint32_t r0 = qp<QP(0, 0, 0, 0)>(r), r1 = qp<QP(1, 1, 1, 1)>(r), r2 = qp<QP(2, 2, 2, 2)>(r),
                            r3 = qp<QP(3, 3, 3, 3)>(r);
@@ -176,10 +202,20 @@ int main(int argc, char** argv) {
     CHK(hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost));
     printf("transpose check: %s\n", bad ? "FAIL" : "ok");
     if (bad) return 1;
+    {   // the LDS-staged quad fetch walks the same chains as the per-lane fetch
+        const size_t n = (size_t)blocks * 256;
+        std::vector<uint32_t> o0(n), o3(n);
+        gather_kernel<0, 0><<<blocks, 256>>>(d_tab, nrec, hot, hot_pct, 50, d_out);
+        CHK(hipMemcpy(o0.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+        gather_kernel<3, 0><<<blocks, 256>>>(d_tab, nrec, hot, hot_pct, 50, d_out);
+        CHK(hipMemcpy(o3.data(), d_out, n * 4, hipMemcpyDeviceToHost));
+        printf("lds-quad chain check: %s\n", o0 == o3 ? "ok" : "FAIL");
+        if (o0 != o3) return 1;
+    }
     printf("nrec %u (%.1f MB) hot %u (%.1f KB) %u%%\n", nrec, nrec * 64.0 / 1e6, hot, hot * 64.0 / 1e3, hot_pct);
-#define ROW(P) printf("pad %3d: lane %.2f quad %.2f quad-noT %.2f Glanesteps/s\n", P, \
+#define ROW(P) printf("pad %3d: lane %.2f quad %.2f quad-noT %.2f quad-lds %.2f Glanesteps/s\n", P, \
         run<0, P>(d_tab, nrec, hot, hot_pct, iters, d_out, blocks), run<1, P>(d_tab, nrec, hot, hot_pct, iters, d_out, blocks), \
-        run<2, P>(d_tab, nrec, hot, hot_pct, iters, d_out, blocks))
+        run<2, P>(d_tab, nrec, hot, hot_pct, iters, d_out, blocks), run<3, P>(d_tab, nrec, hot, hot_pct, iters, d_out, blocks))
     ROW(0); ROW(40); ROW(80); ROW(120);
     return 0;
 }
