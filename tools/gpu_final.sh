@@ -9,7 +9,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=${OUT:-gpurun_out/final}; mkdir -p $O
 export TMPDIR=/tmp
-step() { local name=$1; shift; local t0=$SECONDS; "$@"; local rc=$?; echo "$name rc=$rc ($((SECONDS - t0)) s)"; [ $rc -eq 0 ] || exit $rc; }
+step() { local name=$1; shift; local t0=$SECONDS; "$@"; local rc=$?; echo "$name rc=$rc ($((SECONDS - t0)) s)" >&2; [ $rc -eq 0 ] || exit $rc; }
 if [ -z "$SKIP_TESTS" ]; then
   step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
   step gpu-tests timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
