@@ -78,11 +78,12 @@ def parse():
                          "--stats run whose trace-kernel average is the roofline's exclusive kernel_ms")
     ap.add_argument("--save-image", default="")
     ap.add_argument("--spp", type=int, default=0, help="experiment: samples per step other than the config's 4")
-    ap.add_argument("--iters-per-call", type=int, default=2,
+    ap.add_argument("--iters-per-call", type=int, default=0,
                     help="4-spp iterations per pnrt_render call and per gather of the accumulated rows "
                          "(the primary pass and each launch's drain amortised over them; the image is the "
                          "same); steps stay 4-spp iterations, the last call of the warm-up / the timed "
-                         "region takes what is left")
+                         "region takes what is left.  Default: 2 on one GPU, 4 for a multi-GPU rank, whose "
+                         "share of the frame is smaller (DESIGN.md section 6)")
     ap.add_argument("--kernel-times", action="store_true",
                     help="time every kernel class with HIP events in the timed region (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -141,7 +142,7 @@ def live_pmc(args):
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(v, None)
-    ipc = max(1, args.iters_per_call)
+    ipc = iters_per_call(args, 1)
     steps, warm = 2 * ipc, ipc           # whole calls only: every launch covers ipc iterations
     counters = {}
     try:
@@ -153,7 +154,7 @@ def live_pmc(args):
                    "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
             if args.spp:
                 cmd += ["--spp", str(args.spp)]
-            cmd += ["--iters-per-call", str(args.iters_per_call)]
+            cmd += ["--iters-per-call", str(ipc)]
             log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
             t = time.perf_counter()
             with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
@@ -234,6 +235,18 @@ def cpu_baseline(cfg, target_s: float):
     return cpu, tot
 
 
+def iters_per_call(args, world: int) -> int:
+    """4-spp iterations per pnrt_render call: as given, else 2 on one GPU and 4 for
+    a rank of a multi-GPU run.  A call's primary pass and each trace launch's drain
+    are fixed costs; a rank of N GPUs renders 1/N of the rows, so its calls carry
+    more frames to keep them amortised (one-GPU shard simulation, 16-frame batches:
+    per rank +4 % at N = 2, +3 % at N = 4, +9 % at N = 8 against 8-frame calls; on
+    the whole frame 16-frame calls measured -1 %)."""
+    if args.iters_per_call > 0:
+        return args.iters_per_call
+    return 2 if world == 1 else 4
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,7 +309,7 @@ def main():
     sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
     image = None
 
-    ipc = max(1, args.iters_per_call)
+    ipc = iters_per_call(args, world)
 
     def step(k, lo=0, hi=1 << 30):
         """Iteration k of [lo, hi): the call of its group (ipc iterations from lo,

@@ -179,7 +179,8 @@ static int prof_collect(pnrt_ctx* c) {
 }
 
 #ifndef WF_MAX_CHUNK_FRAMES
-#define WF_MAX_CHUNK_FRAMES 8    // frames per batch at most (a 4-spp call is one batch)
+#define WF_MAX_CHUNK_FRAMES 16   // frames per batch at most (a call of up to four 4-spp iterations of a
+                                 // 1080p frame or share is one batch)
 #endif
 
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {

@@ -3,7 +3,7 @@
 # gather staged through gloo; the gathered image must equal the 1-rank image.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --config C2"
+ARGS=${ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --config C2"}
 timeout -k 10 300 python bench.py $ARGS --save-image gpurun_out/img_n1.npy > gpurun_out/dist_n1.log 2>&1 || exit $?
 NP=${NPROC:-2}
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP --master-addr 127.0.0.1 \
