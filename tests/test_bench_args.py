@@ -1,0 +1,38 @@
+"""bench.py's call shape (CPU): iterations per pnrt_render call by world size,
+and the iteration -> call grouping that times exactly K 4-spp iterations."""
+import importlib.util
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["bench_mod"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_iters_per_call_defaults():
+    b = _bench()
+    ns = type("A", (), {"iters_per_call": 0})()
+    assert b.iters_per_call(ns, 1) == 2           # one GPU: 8-frame calls
+    for n in (2, 4, 8):
+        assert b.iters_per_call(ns, n) == 4       # a multi-GPU rank: 16-frame calls
+    ns.iters_per_call = 3
+    assert b.iters_per_call(ns, 1) == 3 and b.iters_per_call(ns, 8) == 3
+
+
+def test_call_groups_cover_exactly_the_region():
+    """The calls of [lo, hi) render exactly its iterations, in order, none longer
+    than ipc -- for any warm-up / step count and ipc."""
+    b = _bench()
+    for ipc in (1, 2, 3, 4):
+        for lo, hi in ((0, 3), (3, 23), (1, 6), (5, 5), (0, 1), (2, 20)):
+            groups = b.call_groups(lo, hi, ipc)
+            its = [k + i for k, n in groups for i in range(n)]
+            assert its == list(range(lo, hi)), (ipc, lo, hi, groups)
+            assert all(1 <= n <= ipc for _, n in groups)
+            assert len(groups) == -(-(hi - lo) // ipc)

@@ -15,6 +15,10 @@ if [ -z "$SKIP_TESTS" ]; then
   step gpu-tests timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
   tail -3 $O/gpu_tests.log
 fi
+if [ -n "$FUZZ" ]; then   # widened fuzz campaign: FUZZ random scenes x 3 kernel modes vs the oracle
+  step fuzz env PNRT_FUZZ_SEEDS=$FUZZ timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -x -q --timeout 300 --timeout-method thread > $O/fuzz.log 2>&1
+  tail -1 $O/fuzz.log
+fi
 step census timeout -k 10 600 python tools/census.py ${CONFIGS:-C2 C3 C4 C5} > $O/census.log 2>&1
 cp profiles/census.json $O/census.json
 for c in ${CONFIGS:-C2 C3 C4 C5}; do
