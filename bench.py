@@ -247,6 +247,12 @@ def iters_per_call(args, world: int) -> int:
     return 2 if world == 1 else 4
 
 
+def call_groups(lo: int, hi: int, ipc: int):
+    """(first iteration, iterations) of each call covering iterations [lo, hi)
+    exactly: groups of ipc, the last one cut at hi."""
+    return [(k, min(ipc, hi - k)) for k in range(lo, hi, max(1, ipc))]
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -311,16 +317,14 @@ def main():
 
     ipc = iters_per_call(args, world)
 
-    def step(k, lo=0, hi=1 << 30):
-        """Iteration k of [lo, hi): the call of its group (ipc iterations from lo,
-        the group cut at hi) is issued at the group's first iteration."""
-        if (k - lo) % ipc:
-            return
-        n = min(ipc, hi - k)
-        sf.render(spp * k, spp * n)
-        if world > 1:
-            sf.gather_async()                  # one RCCL gather of the row bands to rank 0, overlapped
-                                               # with the next step's rendering
+    def calls(lo, hi):
+        """The pnrt_render calls of iterations [lo, hi): one per group of ipc
+        iterations (the last group cut at hi); multi-GPU ranks gather after each."""
+        for k, n in call_groups(lo, hi, ipc):
+            sf.render(spp * k, spp * n)
+            if world > 1:
+                sf.gather_async()              # one RCCL gather of the row bands to rank 0, overlapped
+                                               # with the next call's rendering
 
     # the library sizes every buffer set at the first call of a size: one untimed call
     # of the timed calls' size first (then the accumulation is reset: the image is the
@@ -329,8 +333,7 @@ def main():
     sf.render(0, spp * ipc)
     torch.cuda.synchronize()
     pt.reset_accum()
-    for k in range(args.warmup):
-        step(k, 0, args.warmup)
+    calls(0, args.warmup)
     if world > 1:
         sf.finish()
     torch.cuda.synchronize()
@@ -338,8 +341,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     if args.child:                             # a PMC pass: the profiler sees the launches; done
-        for k in range(args.steps):
-            step(args.warmup + k, args.warmup, args.warmup + args.steps)
+        calls(args.warmup, args.warmup + args.steps)
         torch.cuda.synchronize()
         pt.close()
         return
@@ -351,8 +353,7 @@ def main():
     pt.profile_select(None if args.kernel_times else [kname])
     pt.profile_enable(True)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k, args.warmup, args.warmup + args.steps)
+    calls(args.warmup, args.warmup + args.steps)
     if world > 1:
         image = sf.finish()                    # every gather completes inside the timed region
     torch.cuda.synchronize()
