@@ -82,8 +82,8 @@ def parse():
                     help="4-spp iterations per pnrt_render call and per gather of the accumulated rows "
                          "(the primary pass and each launch's drain amortised over them; the image is the "
                          "same); steps stay 4-spp iterations, the last call of the warm-up / the timed "
-                         "region takes what is left.  Default: 2 on one GPU, 4 for a multi-GPU rank, whose "
-                         "share of the frame is smaller (DESIGN.md section 6)")
+                         "region takes what is left.  Default: 4 (16 frames) where they fit one batch, "
+                         "else 2 (a whole 4K frame); DESIGN.md section 6")
     ap.add_argument("--kernel-times", action="store_true",
                     help="time every kernel class with HIP events in the timed region (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -142,8 +142,10 @@ def live_pmc(args):
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(v, None)
-    ipc = iters_per_call(args, 1)
-    steps, warm = 2 * ipc, ipc           # whole calls only: every launch covers ipc iterations
+    # whole calls only, so every launch covers the same iterations (the child picks
+    # its own calls: a multiple of 4 iterations is whole calls of 1, 2 or 4)
+    ipc = args.iters_per_call if args.iters_per_call > 0 else 4
+    steps, warm = 2 * ipc, ipc
     counters = {}
     try:
         for i, group in enumerate(PMC_PASSES):
@@ -154,7 +156,7 @@ def live_pmc(args):
                    "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
             if args.spp:
                 cmd += ["--spp", str(args.spp)]
-            cmd += ["--iters-per-call", str(ipc)]
+            cmd += ["--iters-per-call", str(args.iters_per_call)]
             log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
             t = time.perf_counter()
             with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
@@ -235,16 +237,18 @@ def cpu_baseline(cfg, target_s: float):
     return cpu, tot
 
 
-def iters_per_call(args, world: int) -> int:
-    """4-spp iterations per pnrt_render call: as given, else 2 on one GPU and 4 for
-    a rank of a multi-GPU run.  A call's primary pass and each trace launch's drain
-    are fixed costs; a rank of N GPUs renders 1/N of the rows, so its calls carry
-    more frames to keep them amortised (one-GPU shard simulation, 16-frame batches:
-    per rank +4 % at N = 2, +3 % at N = 4, +9 % at N = 8 against 8-frame calls; on
-    the whole frame the bench measures the two the same)."""
+def iters_per_call(args, paths_per_frame: int) -> int:
+    """4-spp iterations per pnrt_render call: as given, else as many as fit one
+    batch, at most 4 (16 frames; a batch holds at most 16 frames and 2^26 path
+    slots: 1080p frames and multi-GPU shares 4, a whole 4K frame 2).  A call's
+    primary pass and each trace launch's drain are fixed costs, and a rank of N
+    GPUs renders 1/N of the rows: against 8-frame calls the one-GPU shard
+    simulation gives per rank +4 % at N = 2, +3 % at N = 4, +9 % at N = 8; on the
+    whole 1080p frame (N = 1) the two measure the same within 1 %."""
     if args.iters_per_call > 0:
         return args.iters_per_call
-    return 2 if world == 1 else 4
+    frames = min(16, (1 << 26) // max(1, paths_per_frame))
+    return max(1, min(4, frames // 4))
 
 
 def call_groups(lo: int, hi: int, ipc: int):
@@ -315,7 +319,7 @@ def main():
     sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
     image = None
 
-    ipc = iters_per_call(args, world)
+    ipc = iters_per_call(args, sf.my_rows * W)
 
     def calls(lo, hi):
         """The pnrt_render calls of iterations [lo, hi): one per group of ipc
