@@ -334,9 +334,10 @@ def main():
     # of the timed calls' size first (then the accumulation is reset: the image is the
     # warm-up's and timed steps' frames as before), so that no later call -- a shorter
     # warm-up call included -- reallocates inside the warm-up or the timed region
-    sf.render(0, spp * ipc)
-    torch.cuda.synchronize()
-    pt.reset_accum()
+    if not args.child:                         # (a PMC pass's warm-up is whole calls: it sizes them,
+        sf.render(0, spp * ipc)                # and its launch counts stay those of its steps)
+        torch.cuda.synchronize()
+        pt.reset_accum()
     calls(0, args.warmup)
     if world > 1:
         sf.finish()
