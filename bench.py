@@ -84,6 +84,8 @@ def parse():
                          "same); steps stay 4-spp iterations, the last call of the warm-up / the timed "
                          "region takes what is left.  Default: 4 (16 frames) where they fit one batch, "
                          "else 2 (a whole 4K frame); DESIGN.md section 6")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="experiment: no HIP events around launches in the timed region")
     ap.add_argument("--kernel-times", action="store_true",
                     help="time every kernel class with HIP events in the timed region (default: only the dominant kernel)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -356,7 +358,7 @@ def main():
     # between launches of the overlapped calls)
     kname = {"v1": "v1", "v3": "trace"}[args.kernel]
     pt.profile_select(None if args.kernel_times else [kname])
-    pt.profile_enable(True)
+    pt.profile_enable(not args.no_kernel_events)
     t0 = time.perf_counter()
     calls(args.warmup, args.warmup + args.steps)
     if world > 1:
@@ -368,7 +370,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = pt.profile_read()
     pt.profile_enable(False)
-    k_ms_total, k_launches = prof[kname]
+    k_ms_total, k_launches = prof.get(kname, (0.0, 0))
     kern_ms_pipe = k_ms_total / max(k_launches, 1)             # average launch duration, pipelined
     launches_per_step = k_launches / args.steps
 
