@@ -16,6 +16,20 @@ PN_DEV float sobol_dev(uint32_t d, uint32_t i) {
         if ((i & 1u) != 0) result ^= c_sobolV[(j + offset) & 255u];
     return (float)result * (1.0f / (float)0xFFFFFFFFu);
 }
+// sobol_dev(d, i) and sobol_dev(d + 1, i) in one pass over the set bits of i only
+// (the same XOR of the same table words: the same bits)
+PN_DEV void sobol_pair(uint32_t d, uint32_t i, float& a, float& b) {
+    uint32_t ra = 0, rb = 0;
+    const uint32_t oa = d * 32u, ob = oa + 32u;
+    while (i != 0) {
+        const uint32_t j = (uint32_t)__builtin_ctz(i);
+        i &= i - 1u;
+        ra ^= c_sobolV[(j + oa) & 255u];
+        rb ^= c_sobolV[(j + ob) & 255u];
+    }
+    a = (float)ra * (1.0f / (float)0xFFFFFFFFu);
+    b = (float)rb * (1.0f / (float)0xFFFFFFFFu);
+}
 
 // ---- per-lane path state --------------------------------------------------------------
 struct Hit {      // Interaction (:60-67) of an accepted triangle

@@ -260,13 +260,16 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
 #ifndef WF_GEN_EARLY
 #define WF_GEN_EARLY 2      // gen: the env table taps fetched with the light record and the material
 #endif
+#ifndef WF_SOBOL_PAIR
+#define WF_SOBOL_PAIR 1     // both Sobol dimensions of a bounce in one pass over the set bits:
+#endif                      // bit 0 in the shade kernel's setup, bit 1 in gen's
 #ifndef WF_SHADE_EARLY
 #define WF_SHADE_EARLY 1    // shade: the light record with the material, the env taps later (registers)
 #endif
 // EARLY 1: the light record is fetched with the material; 2: the env table taps too.
 // Returns the ray kinds the bounce emits; writes the path state P0-P6 of entry
 // i of the write set (slot = the path's (pixel, frame) slot); the rays go to `rays`.
-template <int EARLY>
+template <int EARLY, bool SOBOL_PAIR>
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t slot,
                               int bounce, int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const PathSet& w = b.wr;
@@ -348,7 +351,13 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
     float cpu = rand01(pseed), cpv = rand01(pseed);
     const uint32_t g = (frame + 1u) ^ ((frame + 1u) >> 1);
-    float su = sobol_dev(2u * (uint32_t)bounce, g), sv = sobol_dev(2u * (uint32_t)bounce + 1u, g);
+    float su, sv;
+    if constexpr (SOBOL_PAIR) {
+        sobol_pair(2u * (uint32_t)bounce, g, su, sv);
+    } else {
+        su = sobol_dev(2u * (uint32_t)bounce, g);
+        sv = sobol_dev(2u * (uint32_t)bounce + 1u, g);
+    }
     su += cpu; if (su > 1) su -= 1; if (su < 0) su += 1;
     sv += cpv; if (sv > 1) sv -= 1; if (sv < 0) sv += 1;
     float rDiffuse = 1.0f - m.metallic;
@@ -509,7 +518,7 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
     const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);    // compacted path entry
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core<WF_GEN_EARLY>(s, fp, b, j, i, 0, x, py, frame, q, rays);
+    if (cont) nfl = wf_setup_core<WF_GEN_EARLY, (WF_SOBOL_PAIR & 2) != 0>(s, fp, b, j, i, 0, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
     wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
 }
@@ -1107,7 +1116,7 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core<WF_SHADE_EARLY>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
+    if (cont) nfl = wf_setup_core<WF_SHADE_EARLY, (WF_SOBOL_PAIR & 1) != 0>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
     if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
     wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
 }
