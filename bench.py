@@ -53,6 +53,11 @@ sys.path.insert(0, REPO)
 BAND = 8
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 (8 XCDs) ~34.5 TB/s
+# FETCH_SIZE (KiB) -> fabric read bytes.  MI355X_MICROARCH.md: gfx950's FETCH_SIZE counts
+# half the bytes of wide coalesced reads; the factor for the trace kernel's scattered 64-B
+# gathers is calibrated by tools/microtests/gather_pmc (profiles/r03/fetch_calibration.json)
+FETCH_FACTOR = 2.0
+FETCH_FACTOR_SOURCE = "MI355X_MICROARCH.md; 64-B gather calibration in profiles/r03/fetch_calibration.json"
 # rocprofv3 --pmc passes (one run each; TCC block: FETCH_SIZE uses 3 counters, WRITE_SIZE 2)
 PMC_PASSES = [("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum")]
 KSHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
@@ -178,7 +183,7 @@ def live_pmc(args):
     for k, cs in counters.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
-        e = {"bytes_per_launch": (2.0 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0,
+        e = {"bytes_per_launch": (FETCH_FACTOR * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0,
              "launches_per_step": cs["_n"] / (steps + warm)}
         if "TCC_HIT_sum" in cs:
             e["l2_hit_rate"] = cs["TCC_HIT_sum"] / max(cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"], 1.0)
@@ -198,15 +203,34 @@ def stored_keyed(path, key, src_hash):
 
 
 # ---- CPU baseline ------------------------------------------------------------------------------
+def host_cpus():
+    """(usable, facts): the CPUs this process may run on -- its affinity mask,
+    capped by a cgroup v2 CPU quota when one is set (the GPU box gives a job a
+    share of a larger host: nproc shows every CPU of the machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return usable, {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(cfg, target_s: float):
     """CPU oracle (the C restatement of ray_tracing.comp, OpenMP over rows) on
     whole 1080p 4-spp iterations of the same workload until ~target_s, plus C1
-    (the reference's CPU-runnable config) at full size; returns (dict, counters)."""
+    (the reference's CPU-runnable config) at full size, on every CPU the process
+    may use (host_cpus); returns (dict, counters)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
     from pnraytracing_amd import scenes
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 64))
+    threads, cpu_facts = host_cpus()
     o = pyoracle.Oracle(cfg)
     H = cfg.height
     acc = np.zeros((H, cfg.width, 4), np.float32)
@@ -233,23 +257,25 @@ def cpu_baseline(cfg, target_s: float):
     cpu = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
            "sample": f"{cfg.name}: {it} full {cfg.width}x{H} iterations x {cfg.spp} spp = {n} samples "
                      f"in {dt:.1f}s, oracle/pn_oracle.c OpenMP {threads} threads",
-           "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+           "cpu_model": cpu_model(), **cpu_facts,
            "c1": {"value": round(f1 * c1.width * c1.height / d1 / 1e6, 4), "unit": "Msamples/s",
                   "sample": f"C1 256x256 x {f1} frames (1 spp each, depth 4) in {d1:.2f}s"}}
     return cpu, tot
 
 
-def iters_per_call(args, paths_per_frame: int) -> int:
+def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26) -> int:
     """4-spp iterations per pnrt_render call: as given, else as many as fit one
     batch, at most 4 (16 frames; a batch holds at most 16 frames and 2^26 path
-    slots: 1080p frames and multi-GPU shares 4, a whole 4K frame 2).  A call's
+    slots: 1080p frames and multi-GPU shares 4, a whole 4K frame 2).  Multi-rank
+    runs pass the LARGEST share (ShardedFrame.max_rows), so every rank issues the
+    same calls and therefore the same gathers (batch_slots: a test override).  A call's
     primary pass and each trace launch's drain are fixed costs, and a rank of N
     GPUs renders 1/N of the rows: against 8-frame calls the one-GPU shard
     simulation gives per rank +4 % at N = 2, +3 % at N = 4, +9 % at N = 8; on the
     whole 1080p frame (N = 1) the two measure the same within 1 %."""
     if args.iters_per_call > 0:
         return args.iters_per_call
-    frames = min(16, (1 << 26) // max(1, paths_per_frame))
+    frames = min(16, batch_slots // max(1, paths_per_frame))
     return max(1, min(4, frames // 4))
 
 
@@ -257,6 +283,56 @@ def call_groups(lo: int, hi: int, ipc: int):
     """(first iteration, iterations) of each call covering iterations [lo, hi)
     exactly: groups of ipc, the last one cut at hi."""
     return [(k, min(ipc, hi - k)) for k in range(lo, hi, max(1, ipc))]
+
+
+def issue_calls(sf, spp: int, lo: int, hi: int, ipc: int, world: int) -> int:
+    """The pnrt_render calls of iterations [lo, hi): one per group of ipc
+    iterations (the last group cut at hi); multi-GPU ranks start one gather of
+    their rows after each (overlapped with the next call).  Returns the gathers
+    issued -- a collective, so every rank must issue the same number."""
+    n = 0
+    for k, m in call_groups(lo, hi, ipc):
+        sf.render(spp * k, spp * m)
+        if world > 1:
+            sf.gather_async()
+            n += 1
+    return n
+
+
+def same_on_all_ranks(values, device) -> None:
+    """Raise unless every rank holds the same integers (one all_reduce of
+    (v, -v) with MAX): the call plan of a multi-rank run, checked before any
+    gather is issued -- ranks issuing different numbers of gathers would hang."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor([int(x) for x in values] + [-int(x) for x in values], dtype=torch.int64, device=device)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    k = len(values)
+    if v[:k].tolist() != [int(x) for x in values] or (-v[k:]).tolist() != [int(x) for x in values]:
+        raise SystemExit(f"rank {dist.get_rank()}: call plan {list(values)} differs across ranks "
+                         f"(max {v[:k].tolist()}, min {(-v[k:]).tolist()})")
+
+
+def launches_per_step_of(k_launches: int, steps: int, excl: dict, kname: str):
+    """Dominant-kernel launches per step: from the timed region's events, else from
+    the PNRT_SERIAL steps (same call sizes), else unknown (None)."""
+    if k_launches:
+        return k_launches / steps
+    if kname in excl and excl[kname].get("launches_per_step"):
+        return excl[kname]["launches_per_step"]
+    return None
+
+
+def derive_bound(hbm_frac, l2_hit, l2_frac):
+    """The roof that binds, from the counters: HBM when the kernel's fabric
+    traffic is at least half the HBM peak, or when most L2 lookups miss and the
+    HBM fraction exceeds the L2 one; otherwise the kernel is bound by dependent
+    L1/L2-hit fetch latency."""
+    if hbm_frac is None:
+        return None
+    if hbm_frac >= 0.5 or (l2_hit is not None and l2_hit < 0.6 and (l2_frac is None or hbm_frac >= l2_frac)):
+        return "hbm"
+    return "l2-latency"
 
 
 def main():
@@ -321,16 +397,15 @@ def main():
     sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
     image = None
 
-    ipc = iters_per_call(args, sf.my_rows * W)
+    # every rank plans its calls from the LARGEST share, so all issue the same gathers
+    ipc = iters_per_call(args, sf.max_rows * W)
+    if world > 1:
+        same_on_all_ranks([ipc, len(call_groups(0, args.warmup, ipc)),
+                           len(call_groups(args.warmup, args.warmup + args.steps, ipc))],
+                          "cuda" if args.backend == "nccl" else "cpu")
 
     def calls(lo, hi):
-        """The pnrt_render calls of iterations [lo, hi): one per group of ipc
-        iterations (the last group cut at hi); multi-GPU ranks gather after each."""
-        for k, n in call_groups(lo, hi, ipc):
-            sf.render(spp * k, spp * n)
-            if world > 1:
-                sf.gather_async()              # one RCCL gather of the row bands to rank 0, overlapped
-                                               # with the next call's rendering
+        return issue_calls(sf, spp, lo, hi, ipc, world)
 
     # the library sizes every buffer set at the first call of a size: one untimed call
     # of the timed calls' size first (then the accumulation is reset: the image is the
@@ -371,8 +446,7 @@ def main():
     prof = pt.profile_read()
     pt.profile_enable(False)
     k_ms_total, k_launches = prof.get(kname, (0.0, 0))
-    kern_ms_pipe = k_ms_total / max(k_launches, 1)             # average launch duration, pipelined
-    launches_per_step = k_launches / args.steps
+    kern_ms_pipe = k_ms_total / k_launches if k_launches else None   # average launch duration, pipelined
 
     if args.save_image and rank == 0:
         img = (image.cpu().numpy() if world > 1 else pt.read_accum())
@@ -393,11 +467,12 @@ def main():
         excl = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / (args.serial_steps * ipc)}
                 for k, (ms, n) in ser.items() if n}
     kern_ms = excl[kname]["ms_per_launch"] if kname in excl else None
+    launches_per_step = launches_per_step_of(k_launches, args.steps, excl, kname)
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms_pipe, kern_ms or 0.0], dtype=torch.float64,
+        t = torch.tensor([elapsed, kern_ms_pipe or 0.0, kern_ms or 0.0], dtype=torch.float64,
                          device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_pipe, kern_ms = float(t[0]), float(t[1]), (float(t[2]) or None)
+        elapsed, kern_ms_pipe, kern_ms = float(t[0]), (float(t[1]) or None), (float(t[2]) or None)
 
     samples = W * H * spp * args.steps
     value = samples / elapsed / 1e6
@@ -423,7 +498,7 @@ def main():
         samples_per_step = rows0 * W * spp
         src_hash = build.device_source_hash()
         ref_bytes = None
-        if counts:
+        if counts and launches_per_step:
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import pyoracle
             per = (pyoracle.bounce_traversal_bytes(counts) if args.kernel == "v3"
@@ -435,20 +510,25 @@ def main():
         step_traffic = None
         if pmc and kname in pmc:
             traffic, l2hit = pmc[kname]["bytes_per_launch"], pmc[kname].get("l2_hit_rate")
-            traffic_src = "live rocprofv3 --pmc (FETCH_SIZE; WRITE_SIZE + TCC_HIT/MISS), 2 x FETCH_SIZE + WRITE_SIZE"
+            traffic_src = (f"live rocprofv3 --pmc (FETCH_SIZE; WRITE_SIZE + TCC_HIT/MISS), {FETCH_FACTOR:g} x FETCH_SIZE "
+                           f"+ WRITE_SIZE ({FETCH_FACTOR_SOURCE})")
             step_traffic = {k: {"bytes_per_launch": round(e["bytes_per_launch"]),
                                 "launches_per_step": round(e["launches_per_step"], 3),
                                 "l2_hit_rate": round(e["l2_hit_rate"], 4) if "l2_hit_rate" in e else None}
                             for k, e in pmc.items()}
             step_traffic["total_bytes_per_step"] = round(sum(e["bytes_per_launch"] * e["launches_per_step"]
                                                              for e in pmc.values()))
-        elif world == 1:
+        else:
+            # no live PMC here (N > 1: the passes run at N = 1 only): the N = 1 live
+            # figure recorded for these sources (tools/record_pmc.py), scaled to this
+            # rank's launch -- its share of the rows and its frames per launch
             e = stored_keyed("pmc.json", f"{cfg.name}/{kname}", src_hash)
-            if e and e.get("hbm_bytes_per_launch"):
-                traffic, l2hit = e["hbm_bytes_per_launch"], e.get("l2_hit_rate")
-                traffic_src = "profiles/pmc.json (recorded for these sources)"
-        if traffic is not None and world > 1:
-            traffic = None                     # PMC is per-process at N = 1 only
+            if e and e.get("bytes_per_launch"):
+                scale = rows0 / e["rows"] * (spp * ipc) / e["frames_per_launch"]
+                traffic, l2hit = e["bytes_per_launch"] * scale, e.get("l2_hit_rate")
+                traffic_src = (f"derived: N = 1 live PMC recorded for these sources (profiles/pmc.json, "
+                               f"{e['bytes_per_launch']:.4g} B per {e['frames_per_launch']}-frame launch of "
+                               f"{e['rows']} rows) x this rank's share ({rows0} rows, {spp * ipc} frames)")
         achieved = traffic / (kern_ms * 1e-3) / 1e9 if (traffic and kern_ms) else None
         census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
         requested = None
@@ -460,7 +540,7 @@ def main():
                          "frac_of_l2": round(rb / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
                          "source": "profiles/census.json (WF_STATS build of these sources)"}
         checks = None
-        if kern_ms:
+        if kern_ms and launches_per_step:
             checks = {"launches_x_kernel_ms": round(launches_per_step * kern_ms, 4),
                       "le_ms_per_step": launches_per_step * kern_ms <= elapsed / args.steps * 1e3,
                       "frac_le_1": (achieved / HBM_PEAK_GBS <= 1.0) if achieved else None}
@@ -478,15 +558,20 @@ def main():
                        "iters_per_call": ipc,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
                        "kernel": kfull},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
+            "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
+                                               requested["frac_of_l2"] if requested else None),
+                         "bound_rule": "derived from the counters (bench.derive_bound): hbm if frac >= 0.5, or "
+                                       "if l2_hit_rate < 0.6 and frac >= requested.frac_of_l2; else l2-latency "
+                                       "(dependent L1/L2-hit fetch chains); peak / frac stay against HBM",
+                         "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "l2_hit_rate": round(l2hit, 4) if l2hit is not None else None,
                          "kernel": kfull, "kernel_ms": kern_ms, "kernel_ms_timing": "exclusive (PNRT_SERIAL steps)",
-                         "kernel_ms_pipelined": round(kern_ms_pipe, 4), "launches_per_step": launches_per_step,
+                         "kernel_ms_pipelined": round(kern_ms_pipe, 4) if kern_ms_pipe else None,
+                         "launches_per_step": launches_per_step,
                          "checks": checks,
-                         "limiter": "dependent-fetch latency (L1-hit chains), not HBM: DESIGN.md section 4",
                          "requested": requested,
                          "reference_bytes_per_launch": ref_bytes},
             "kernels": kernels,

@@ -28,6 +28,12 @@ extern "C" {
 #define PNRT_E_STATE (-3)     /* call out of order (e.g. render before upload) */
 #define PNRT_E_SCENE (-4)     /* scene arrays inconsistent / unsupported */
 #define PNRT_E_NOMEM (-5)
+#define PNRT_E_TRACE (-6)     /* a trace launch may have left queued rays untraced (a bounded */
+                              /* wait of its ray queue ran out, or a ray count check failed): */
+                              /* the accumulation image is invalid.  Returned by pnrt_render,  */
+                              /* pnrt_synchronize, pnrt_read_accum and pnrt_pack_rows once the */
+                              /* faulting work has completed (pnrt_synchronize / read_accum    */
+                              /* always see it); sticky until pnrt_reset_accum.                */
 
 typedef struct pnrt_ctx pnrt_ctx;
 
@@ -118,7 +124,8 @@ int pnrt_set_options(pnrt_ctx* ctx, int options);
 int pnrt_render(pnrt_ctx* ctx, uint32_t first_frame, uint32_t n_frames, int band_rows,
                 int n_shards, int shard);
 
-/* Redraw semantics (main.cpp:592-596): zero the accumulation image. */
+/* Redraw semantics (main.cpp:592-596): zero the accumulation image.  Also
+ * clears a PNRT_E_TRACE fault (it waits for the calls in flight first). */
 int pnrt_reset_accum(pnrt_ctx* ctx);
 /* Synchronise and copy the width*height*4 floats (row 0 = bottom) to host. */
 int pnrt_read_accum(pnrt_ctx* ctx, float* rgba_out);

@@ -75,6 +75,28 @@ def build_device(force=False, extra=()):
     return out
 
 
+# Diagnostic device libraries the GPU tests load in a child process (PNRT_DEVICE_LIB):
+# never the product library (pnrt_version() says DIAGNOSTIC BUILD).
+#   guard1  the trace kernel's block-queue claim gives up after one attempt, so
+#           queued rays go untraced: pnrt_* must report PNRT_E_TRACE
+DIAG_VARIANTS = {"guard1": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_GUARD=1"]}
+
+
+def variant_path(name: str) -> str:
+    return os.path.join(PKG, "variants", f"libpnrt_{name}.so")
+
+
+def build_diag_variants(force=False):
+    deps = [os.path.join(CSRC, d) for d in DEVICE_DEPS] + [os.path.join(INC, "pnrt.h")]
+    os.makedirs(os.path.join(PKG, "variants"), exist_ok=True)
+    for name, flags in DIAG_VARIANTS.items():
+        out = variant_path(name)
+        if force or _stale(out, deps):
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+                  "-fno-fast-math", "-fno-gpu-rdc", "-fno-slp-vectorize", f'-DPNRT_SRC_HASH="{device_source_hash()}"',
+                  "-I", INC, *flags, *[os.path.join(CSRC, s) for s in DEVICE_SRCS], "-o", out])
+
+
 def build_abi_caller(force=False):
     """tests/abi/c_abi_render: a compiled C++ caller of include/pnrt.h +
     include/pnrt_host.h linked against the two libraries (TEST-ONLY; exercises
@@ -102,6 +124,7 @@ def build_oracle(force=False):
 def build_all(force=False):
     build_host(force)
     build_device(force)
+    build_diag_variants(force)
     build_abi_caller(force)
     build_oracle(force)
 

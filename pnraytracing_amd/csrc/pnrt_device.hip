@@ -61,6 +61,12 @@ struct pnrt_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     std::string err;
+    // trace faults (pt_wf.h wf_fault): WF_FAULT_WORDS words in host-mapped memory the
+    // kernels write only when a check trips; `faulted` latches until reset_accum
+    uint32_t* fault_host = nullptr;
+    uint32_t* fault_dev = nullptr;
+    bool faulted = false;
+    std::string fault_msg;
     // scene
     std::vector<void*> scene_allocs;
     DevScene scene{};
@@ -126,6 +132,25 @@ struct pnrt_ctx {
 static int set_err(pnrt_ctx* c, int code, const std::string& m) {
     if (c) c->err = m;
     return code;
+}
+
+// PNRT_E_TRACE once a fault word is set by completed work (see pnrt.h)
+static int check_fault(pnrt_ctx* c) {
+    if (!c->faulted && c->fault_host) {
+        static const char* what[WF_FAULT_WORDS] = {
+            "a bounded wait of the trace kernel's block ray queue ran out",
+            "a trace block loaded fewer rays than it dequeued",
+            "a trace launch ended with ray-queue items never dequeued", "?"};
+        std::string m;
+        for (int k = 0; k < WF_FAULT_WORDS; ++k)
+            if (__atomic_load_n(c->fault_host + k, __ATOMIC_ACQUIRE)) m += (m.empty() ? "" : "; ") + std::string(what[k]);
+        if (!m.empty()) {
+            c->faulted = true;
+            c->fault_msg = "trace fault: " + m + " -- queued rays may be untraced, the accumulation image is "
+                           "invalid (pnrt_reset_accum clears it)";
+        }
+    }
+    return c->faulted ? set_err(c, PNRT_E_TRACE, c->fault_msg) : PNRT_OK;
 }
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
@@ -457,6 +482,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         char* base = static_cast<char*>(P.wf);
         WfLayout a = wf_layout(base, per_frame * cfA);
         a.b.ovf = P.ovf[0];
+        a.b.fault = c->fault_dev;
         a.b.ovf_stride = (uint32_t)ovf_stride;
         a.b.chunk_frames = (int)cfA;
         a.b.tiles_x = tiles_x;
@@ -468,6 +494,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         if (cfB) {
             WfLayout bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
             bb.b.ovf = P.ovf[1];
+            bb.b.fault = c->fault_dev;
             bb.b.ovf_stride = (uint32_t)ovf_stride;
             bb.b.chunk_frames = (int)cfB;
             bb.b.tiles_x = tiles_x;
@@ -524,6 +551,18 @@ int pnrt_create(int device, pnrt_ctx** out) {
         delete c;
         return PNRT_E_HIP;
     }
+    void* fh = nullptr;
+    void* fd = nullptr;
+    if (hipHostMalloc(&fh, 256, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&fd, fh, 0) != hipSuccess) {
+        if (fh) (void)hipHostFree(fh);
+        (void)hipStreamDestroy(c->own_stream);
+        delete c;
+        return PNRT_E_HIP;
+    }
+    std::memset(fh, 0, 256);
+    c->fault_host = static_cast<uint32_t*>(fh);
+    c->fault_dev = static_cast<uint32_t*>(fd);
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_sobolV), kSobolV, sizeof kSobolV) != hipSuccess) {
         (void)hipStreamDestroy(c->own_stream);
         delete c;
@@ -563,6 +602,7 @@ void pnrt_destroy(pnrt_ctx* c) {
     for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
+    if (c->fault_host) (void)hipHostFree(c->fault_host);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -949,6 +989,7 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
     if (!c) return PNRT_E_ARG;
     if (!c->has_scene || !c->has_frame) return set_err(c, PNRT_E_STATE, "render: upload_scene and set_frame first");
     if (band < 1 || nsh < 1 || shard < 0 || shard >= nsh) return set_err(c, PNRT_E_ARG, "render: bad shard selector");
+    if (int rc = check_fault(c)) return rc;      // an earlier call's trace fault (completed work)
     if (nf == 0) return PNRT_OK;
     HIPCHK(c, hipSetDevice(c->device));
     FrameParams fp;
@@ -986,8 +1027,15 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
 
 int pnrt_reset_accum(pnrt_ctx* c) {
     if (!c) return PNRT_E_ARG;
-    if (!c->accum) return PNRT_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    (void)check_fault(c);
+    if (c->faulted) {                 // a new accumulation: wait for the calls in flight, clear the fault
+        HIPCHK(c, sync_all(c));
+        for (int k = 0; k < WF_FAULT_WORDS; ++k) __atomic_store_n(c->fault_host + k, 0u, __ATOMIC_RELEASE);
+        c->faulted = false;
+        c->fault_msg.clear();
+    }
+    if (!c->accum) return PNRT_OK;
     HIPCHK(c, hipMemsetAsync(c->accum, 0, (size_t)c->width * c->height * 16, c->stream));
     return PNRT_OK;
 }
@@ -998,7 +1046,7 @@ int pnrt_read_accum(pnrt_ctx* c, float* out) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(out, c->accum, (size_t)c->width * c->height * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, sync_all(c));
-    return PNRT_OK;
+    return check_fault(c);
 }
 
 void* pnrt_accum_device_ptr(pnrt_ctx* c) { return c ? c->accum : nullptr; }
@@ -1031,6 +1079,7 @@ int pnrt_pack_rows(pnrt_ctx* c, void* dst, int band, int nsh, int shard) {
     if (!c || !dst) return PNRT_E_ARG;
     if (!c->accum) return set_err(c, PNRT_E_STATE, "pack_rows: no frame");
     if (band < 1 || nsh < 1 || shard < 0 || shard >= nsh) return set_err(c, PNRT_E_ARG, "pack_rows: bad shard selector");
+    if (int rc = check_fault(c)) return rc;      // completed work that faulted
     HIPCHK(c, hipSetDevice(c->device));
     int rows = shard_rows(c->height, band, nsh, shard);
     size_t total = (size_t)rows * c->width;
@@ -1045,7 +1094,7 @@ int pnrt_synchronize(pnrt_ctx* c) {
     if (!c) return PNRT_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, sync_all(c));
-    return PNRT_OK;
+    return check_fault(c);
 }
 
 int pnrt_get_device_info(pnrt_ctx* c, pnrt_device_info* info) {

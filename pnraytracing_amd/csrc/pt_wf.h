@@ -53,6 +53,11 @@
 #define WF_SPA_STRIDE (WF_TRACE_BLOCK * 8u)                 // LDS bytes per stack depth
 #define WF_SPA_SHIFT (WF_TRACE_BLOCK == 512 ? 12 : WF_TRACE_BLOCK == 256 ? 11 : 10)
 #define WF_CHUNK 256u        // rays per dequeue
+#ifndef WF_SUB
+#define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
+#endif
+#define WF_NSUB (256 / WF_SUB)
+#define WF_BQ_GUARD (WF_DIAG_GUARD > 0 ? (uint32_t)WF_DIAG_GUARD : (1u << 10))   // block-queue claim attempts
 #ifndef WF_CONT_FROM_STATE
 #define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued
 #endif
@@ -148,14 +153,37 @@ struct WfBufs {
     uint32_t npad;           // n rounded up to 256
     uint32_t nseg_k;         // setup blocks = segments per kind
     unsigned long long* stats; // WF_STATS builds: traversal step census (8 counters)
+    uint32_t* fault;   // the context's fault words (host-mapped, see wf_fault), WF_FAULT_* index
     uint32_t n;        // path slots
     int chunk_frames;
     int tiles_x;
     uint32_t first_frame;
 };
 
+// Faults: a trace launch that could leave a queued ray untraced reports it
+// instead of returning a silently wrong image (ray_tracing.comp:429-494 traces
+// every ray).  One word per kind in the context's host-mapped fault area,
+// written with a system-scope vector store only when a check trips (pnrt_render,
+// pnrt_synchronize, pnrt_read_accum and pnrt_pack_rows then return PNRT_E_TRACE).
+#define WF_FAULT_GUARD 0     // a bounded wait of the block-level ray queue ran out
+#define WF_FAULT_BLOCK 1     // a trace block loaded fewer rays than it dequeued
+#define WF_FAULT_DRAIN 2     // a trace launch ended with queue items never dequeued
+#define WF_FAULT_WORDS 4
+PN_DEV void wf_fault(const WfBufs& b, int kind) {
+    __hip_atomic_store(b.fault + kind, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // A setup kernel's block 0 resets the dequeue counters of the trace launch that
-// follows it (the previous trace has completed: stream order).
+// follows it (the previous trace has completed: stream order).  The shade
+// kernels first check that the previous trace handed out every queue item: item
+// i is ticket i / WF_QSHARDS of counter i % WF_QSHARDS, so counter p must have
+// passed all ceil((nseg - p) / WF_QSHARDS) tickets below nseg.
+PN_DEV void wf_check_drained(const WfBufs& b) {
+    if (blockIdx.x == 0 && threadIdx.x < WF_QSHARDS) {
+        const uint32_t nseg = 3u * b.nseg_k * WF_NSUB, p = threadIdx.x;
+        const uint32_t need = nseg > p ? (nseg - p + WF_QSHARDS - 1) / WF_QSHARDS : 0u;
+        if (b.counter[p * WF_QSTRIDE] < need) wf_fault(b, WF_FAULT_DRAIN);
+    }
+}
 PN_DEV void wf_reset_counters(const WfBufs& b) {
     if (blockIdx.x == 0 && threadIdx.x < WF_QSHARDS) b.counter[threadIdx.x * WF_QSTRIDE] = 0u;
 }
@@ -605,10 +633,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_BQ_PREFETCH
 #define WF_BQ_PREFETCH 0    // block queue: fetch the next segment when fewer rays than this remain (0 = off)
 #endif
-#ifndef WF_SUB
-#define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
-#endif
-#define WF_NSUB (256 / WF_SUB)
 #ifndef WF_KIND_ORDER
 #define WF_KIND_ORDER 0x210 // sweep order of the ray kinds, one hex digit each (0 light, 1 env, 2 continuation)
 #endif
@@ -748,7 +772,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         if (threadIdx.x < 48) hist[threadIdx.x] = 0u;
         __syncthreads();
     }
-    uint32_t n_rays = 0;
     uint32_t next = 0, end = 0, ckind = 0, qpart = 0;
     bool exhausted = false;
 
@@ -761,6 +784,18 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     t.any = true;
     uint32_t rid = 0;
     int busy = 0;
+    // Ray accounting: when the block's last wave leaves, every ray the block took
+    // off the global queue must have been loaded into a lane (a loaded ray is always
+    // traced: the loop below ends only with no lane busy).  Block queue: generations
+    // advance only once a segment is fully claimed, and claimed rays are loaded at
+    // once (a wave claims as many as it has idle lanes), so the check is that the
+    // current generation's segment is used up.  Per-wave queue: bk_cnt[0] = rays
+    // dequeued - rays loaded.  bk_cnt[1] counts the waves that have left.
+    __shared__ uint32_t bk_cnt[2];
+    if (!WF_BLOCKQ) {
+        if (threadIdx.x == 0) bk_cnt[0] = bk_cnt[1] = 0u;
+        __syncthreads();
+    }
     uint64_t last_ray = 0;      // WF_TIMING builds: (iteration, kind, lane steps) of the lane's last finished ray
     uint32_t witer = 0, witer_exh = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
@@ -796,6 +831,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             const uint32_t lo = min(part * (uint32_t)WF_SUB, cnt);
             next = ckind * b.npad + j * 256u + lo;
             end = ckind * b.npad + j * 256u + min(lo + (uint32_t)WF_SUB, cnt);
+            if (!WF_BLOCKQ && lane == 0) atomicAdd(&bk_cnt[0], end - next);   // ray accounting (below)
         }
     };
 #if WF_BLOCKQ
@@ -814,6 +850,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     if (threadIdx.x == 0) {
         bq_claim = 0u; bq_refill = 0u; bq_done = 0u; bq_pf = 0u; bq_pf_done = 0u;
         bq_seg[0][0] = bq_seg[0][1] = 0u; bq_seg[0][2] = 0u;
+        bk_cnt[0] = bk_cnt[1] = 0u;
     }
     __syncthreads();
     // the next non-empty global segment into next / end / ckind, or exhausted
@@ -823,7 +860,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         } while (!exhausted && next >= end);
     };
     auto bclaim = [&](uint32_t want) {
-        for (uint32_t guard = 0; guard < (1u << 10); ++guard) {
+        for (uint32_t guard = 0; guard < WF_BQ_GUARD; ++guard) {
             uint32_t c = 0;
             if (lane == 0) c = __hip_atomic_fetch_add(&bq_claim, want, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             c = __builtin_amdgcn_readfirstlane(c);
@@ -901,7 +938,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 __builtin_amdgcn_s_sleep(2);
             }
         }
-        exhausted = true;                       // guard: never expected
+        exhausted = true;                       // guard: never expected -- reported, never silent
+        if (lane == 0) wf_fault(b, WF_FAULT_GUARD);
     };
 #endif
     // one traversal step of a busy lane, the result stored when its ray is done
@@ -960,6 +998,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
             if (idle != 0 && next < end) {
                 const uint32_t myid = next + lanes_below(idle);
+                if (!WF_BLOCKQ && lane == 0) atomicSub(&bk_cnt[0], min((uint32_t)__popcll(idle), end - next));
                 next = min(next + (uint32_t)__popcll(idle), end);
                 if (busy == 0 && myid < end) {
                     const uint32_t kind = ckind;
@@ -1001,6 +1040,20 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         };
         if (__ballot(busy != 0 && t.r.kz() != 2) == 0) run(std::true_type{});
         else run(std::false_type{});
+    }
+    if (lane == 0) {      // the block's last wave out checks the ray accounting
+        const uint32_t out = __hip_atomic_fetch_add(&bk_cnt[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (out == WF_TRACE_BLOCK / 64 - 1) {
+#if WF_BLOCKQ
+            const uint32_t c = __hip_atomic_load(&bq_claim, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t q = (c >> 16) & 15;
+            const bool lost = (c & 0xffffu) < bq_seg[q][1] - bq_seg[q][0] ||
+                              __hip_atomic_load(&bq_pf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u;
+#else
+            const bool lost = __hip_atomic_load(&bk_cnt[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
+#endif
+            if (lost) wf_fault(b, WF_FAULT_BLOCK);
+        }
     }
     if (WF_TIMING && lane == 0) {      // diagnostic builds: per-wave start / queue-empty / end (100 MHz clock)
         unsigned long long* t = b.stats + 8 + 4 * ((size_t)blockIdx.x * (WF_TRACE_BLOCK / 64) + (threadIdx.x >> 6));
@@ -1049,8 +1102,9 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     const float4 p3 = ps_ld(useL ? rd.P3 + i : s.zero4);
     const float4 p4 = ps_ld(useE ? rd.P4 + i : s.zero4);
     // the continuation hit's records, in flight while the MIS sum waits for P3/P4
-    // (a miss reads triangle 0's, unused)
-    const HitFetch hf = hit_fetch(s, ht < 0 ? 0 : ht);
+    // (a miss reads triangle 0's, unused; so does an index a faulted trace left
+    // stale -- reported as PNRT_E_TRACE, never a wild read)
+    const HitFetch hf = hit_fetch(s, (uint32_t)ht < (uint32_t)s.n_tris ? ht : 0);
     asm volatile("" ::: "memory");     // issue them here (the scheduler would sink them past the MIS wait)
     f3 LD = mk3(p3.x, p3.y, p3.z), LE = mk3(p4.x, p4.y, p4.z);
     float pl = p3.w, pe = p2.w;
@@ -1098,6 +1152,7 @@ template <bool FINAL>
 __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_setup(DevScene s, FrameParams fp, WfBufs b,
                                                                      const float4* primary, float4* colors) {
     // the block's live paths are its first b.rd.bcount[block] entries
+    wf_check_drained(b);                      // (the previous trace's counters, then reset)
     if (!FINAL) wf_reset_counters(b);
     const uint32_t live = b.rd.bcount[blockIdx.x];
     if (live == 0) {                          // no path: nothing to shade, no rays, empty next block

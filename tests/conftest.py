@@ -20,5 +20,6 @@ def _built():
     build.build_host()
     if os.path.exists(build.HIPCC):
         build.build_device()
+        build.build_diag_variants()
     build.build_oracle()
     yield

@@ -44,3 +44,17 @@ def test_device_create_fails_loudly_without_gpu():
     from pnraytracing_amd.tracer import PathTracer, PnrtError
     with pytest.raises(PnrtError):
         PathTracer(0)
+
+
+def test_diag_variant_is_marked_diagnostic():
+    """The fault-injection library the GPU fault test loads (build.DIAG_VARIANTS)
+    exists, exports the same ABI and can never pass for the product library."""
+    from pnraytracing_amd import build
+    path = build.variant_path("guard1")
+    if not os.path.exists(path):
+        pytest.skip("diagnostic variant not built (no hipcc)")
+    lib = ctypes.CDLL(path)
+    missing = [n for n in declared("pnrt.h") if not hasattr(lib, n)]
+    assert not missing, missing
+    lib.pnrt_version.restype = ctypes.c_char_p
+    assert "DIAGNOSTIC BUILD" in lib.pnrt_version().decode()

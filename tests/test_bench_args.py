@@ -39,3 +39,26 @@ def test_call_groups_cover_exactly_the_region():
             assert its == list(range(lo, hi)), (ipc, lo, hi, groups)
             assert all(1 <= n <= ipc for _, n in groups)
             assert len(groups) == -(-(hi - lo) // ipc)
+
+
+def test_launch_count_without_kernel_events():
+    """--no-kernel-events: the timed region records no launches; the launch count
+    comes from the PNRT_SERIAL steps, or is unknown -- never a division by 0."""
+    b = _bench()
+    assert b.launches_per_step_of(16, 4, {}, "trace") == 4.0
+    assert b.launches_per_step_of(0, 4, {"trace": {"ms_per_launch": 3.0, "launches_per_step": 1.0}}, "trace") == 1.0
+    assert b.launches_per_step_of(0, 4, {}, "trace") is None
+
+
+def test_bound_derived_from_counters():
+    b = _bench()
+    assert b.derive_bound(0.16, 0.80, 0.34) == "l2-latency"     # C2: L1/L2-hit chains
+    assert b.derive_bound(0.43, 0.52, 0.20) == "hbm"            # C5: 1 GB scene, half the L2 lookups miss
+    assert b.derive_bound(0.62, 0.90, 0.30) == "hbm"
+    assert b.derive_bound(None, 0.5, 0.3) is None
+
+
+def test_host_cpus_reports_affinity():
+    b = _bench()
+    n, facts = b.host_cpus()
+    assert n >= 1 and facts["affinity_cpus"] >= n and facts["nproc"] >= facts["affinity_cpus"]

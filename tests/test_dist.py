@@ -67,6 +67,60 @@ def test_gather_equals_single_process(tmp_path, world, w, h, band, overlap):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
+def _plan_worker(rank, world, port, w, h, band, slots, spp, warm, steps, out_path):
+    """bench.py's own call planning and call loop on a frame whose largest share
+    crosses the batch threshold while the smaller one does not."""
+    sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "oracle")); sys.path.insert(0, os.path.join(REPO, "tests"))
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from oracle_tracer import OracleTracer
+    from pnraytracing_amd import scenes as S
+    from pnraytracing_amd.dist import ShardedFrame
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        tr = OracleTracer(S.cornell_c1(w, h))
+        sf = ShardedFrame(tr, band=band, device="cpu")
+        ns = type("A", (), {"iters_per_call": 0})()
+        own = [None] * world                      # what each rank would plan from its OWN share
+        dist.all_gather_object(own, bench.iters_per_call(ns, sf.my_rows * w, batch_slots=slots))
+        assert len(set(own)) > 1, own             # the hazard is present in this frame
+        ipc = bench.iters_per_call(ns, sf.max_rows * w, batch_slots=slots)
+        bench.same_on_all_ranks([ipc, len(bench.call_groups(0, warm, ipc)),
+                                 len(bench.call_groups(warm, warm + steps, ipc))], "cpu")
+        n = bench.issue_calls(sf, spp, 0, warm, ipc, world)
+        sf.finish()
+        n += bench.issue_calls(sf, spp, warm, warm + steps, ipc, world)
+        img = sf.finish()
+        counts = [None] * world
+        dist.all_gather_object(counts, n)
+        assert len(set(counts)) == 1, counts      # every rank issued the same gathers
+        if rank == 0:
+            np.save(out_path, img.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_gather_count_same_on_every_rank(tmp_path):
+    """bench.py plans its pnrt_render calls -- and so its gathers -- from the
+    largest share: ranks whose own shares fall on either side of the batch
+    threshold still issue the same number of gathers (a mismatch hangs RCCL), and
+    the gathered image equals one process's render."""
+    import pyoracle
+    from pnraytracing_amd import scenes as S
+    w, h, band, spp, warm, steps = 40, 44, 8, 2, 1, 3
+    slots = 20 * w * 8            # rank 1's 20 rows fit 8 frames (2 iterations), rank 0's 24 only 6 (1)
+    out = str(tmp_path / "img.npy")
+    mp.start_processes(_plan_worker, args=(2, _free_port(), w, h, band, slots, spp, warm, steps, out), nprocs=2,
+                       join=True, start_method="spawn")
+    got = np.load(out)
+    o = pyoracle.Oracle(S.cornell_c1(w, h))
+    ref = np.zeros((h, w, 4), np.float32)
+    o.render(0, spp * (warm + steps), accum=ref)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
 def test_single_rank_without_process_group():
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_tracer import OracleTracer
