@@ -69,7 +69,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5"])
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4", "C5", "D2", "D3"],
+                    help="C2-C5: BASELINE configs; D2 / D3: the C2 / C3 scene at the reference's own dispatch "
+                         "shape -- 512x512 (PnRT.hpp:41-42), 1 spp per frame, one pnrt_render per frame "
+                         "(main.cpp:569-615): a step is one frame")
+    ap.add_argument("--sync-per-frame", action="store_true",
+                    help="D configs: synchronise after every call (an interactive loop that displays each frame)")
     ap.add_argument("--mode", default="zcull", choices=["exact", "zcull"])
     ap.add_argument("--kernel", default="v3", choices=["v1", "v3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
@@ -372,7 +377,13 @@ def main():
 
     builders = {"C2": scenes.bunny_c2, "C3": scenes.marry_c3, "C4": scenes.teapot_c4, "C5": scenes.synthetic_c5}
     t = time.perf_counter()
-    cfg = builders[args.config]()
+    dispatch_shape = args.config.startswith("D")
+    if dispatch_shape:                  # the reference's interactive shape: 512x512, one 1-spp frame per call
+        cfg = builders["C" + args.config[1:]](width=512, height=512, spp=1)
+        cfg.name = args.config + cfg.name[2:] + "@512"
+        args.iters_per_call = 1
+    else:
+        cfg = builders[args.config]()
     scene_s = time.perf_counter() - t
     if args.spp:
         cfg.spp = args.spp
@@ -405,6 +416,12 @@ def main():
                           "cuda" if args.backend == "nccl" else "cpu")
 
     def calls(lo, hi):
+        if args.sync_per_frame:             # every frame completed before the next is submitted
+            n = 0
+            for k in range(lo, hi):
+                n += issue_calls(sf, spp, k, k + 1, ipc, world)
+                torch.cuda.synchronize()
+            return n
         return issue_calls(sf, spp, lo, hi, ipc, world)
 
     # the library sizes every buffer set at the first call of a size: one untimed call
@@ -553,7 +570,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: procedural stand-in meshes (reference OBJs absent), reference HDR/texture assets",
-            "config": {"workload": f"{cfg.name}: {cfg.description}", "width": W, "height": H,
+            "config": {"workload": f"{cfg.name}: {cfg.description}"
+                                   + (" -- reference dispatch shape, one pnrt_render per frame"
+                                      + (", synchronised per frame" if args.sync_per_frame else "")
+                                      if dispatch_shape else ""), "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "iters_per_call": ipc,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",

@@ -110,6 +110,13 @@ def build_abi_caller(force=False):
     if force or _stale(out, deps):
         _run(["g++", "-std=c++17", "-O2", "-Wall", "-I", INC, src, "-o", out, "-L", PKG, "-lpnrt", "-lpnrt_host",
               "-Wl,-rpath,$ORIGIN/../../pnraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib"])
+    # the multi-GPU caller: one process, one RCCL communicator per device (ncclCommInitAll + ncclGather)
+    msrc = os.path.join(REPO, "tests", "abi", "c_abi_multigpu.cpp")
+    mout = os.path.join(REPO, "tests", "abi", "c_abi_multigpu")
+    if os.path.exists(msrc) and (force or _stale(mout, deps[1:] + [msrc])):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", INC, "-I", "/opt/rocm/include", msrc,
+              "-o", mout, "-L", PKG, "-L", "/opt/rocm/lib", "-lpnrt", "-lpnrt_host", "-lamdhip64", "-lrccl",
+              "-Wl,-rpath,$ORIGIN/../../pnraytracing_amd", "-Wl,-rpath,/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib"])
     return out
 
 

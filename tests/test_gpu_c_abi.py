@@ -43,3 +43,27 @@ def test_compiled_caller_renders_c1_bit_exact(tmp_path):
     img = np.fromfile(out, np.float32).reshape(H, W, 4)
     bad = np.argwhere(np.any(img.view(np.uint32) != gold["image"].view(np.uint32), axis=-1))
     assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+
+
+MEXE = os.path.join(HERE, "abi", "c_abi_multigpu")
+
+
+@pytest.mark.parametrize("n_shards", [3, 8])
+def test_compiled_multigpu_caller_gathers_bit_exact(tmp_path, n_shards):
+    """SURVEY 8e's process model in C++: one process,
+    ncclCommInitAll over the visible devices, one pnrt context per row-band
+    shard, pnrt_pack_rows + ncclGather to device 0.  The gathered image equals
+    the single-context render (checked inside the program) and the committed
+    oracle image, bit for bit.  On a one-GPU box the shards share the device."""
+    assert os.path.exists(MEXE), "tests/abi/c_abi_multigpu not built (python -c 'import __graft_entry__ as g; g.build()')"
+    gold = np.load(os.path.join(GOLD, "c1_oracle_image.npz"))
+    H, W = gold["image"].shape[:2]
+    scene, out = str(tmp_path / "c1.bin"), str(tmp_path / "out.bin")
+    write_scene(scene)
+    r = subprocess.run([MEXE, scene, out, str(W), str(H), str(int(gold["frames"])), str(n_shards)], capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bit-identical to the single-context render" in r.stdout, r.stdout
+    img = np.fromfile(out, np.float32).reshape(H, W, 4)
+    bad = np.argwhere(np.any(img.view(np.uint32) != gold["image"].view(np.uint32), axis=-1))
+    assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
