@@ -8,6 +8,10 @@
 //   WF_KO_ENV       knockout: env lookups without math (1) or memory (2)  -- WRONG IMAGES
 //   WF_DIAG_NOSTORE knockout: trace results dropped                       -- WRONG IMAGES
 //   WF_DIAG_VALU    N extra VALU instructions per traversal step (issue-bound probe)
+//   WF_KO_STATE     knockout: the path state the trace does not read (P2-P5: BRDF
+//                   value, MIS candidates, Lo, seed) neither stored by the setups nor
+//                   loaded by the shade -- register stand-ins; P0 / P1 / P7 (the
+//                   rays) and P6 (throughput, meta: control flow) kept -- WRONG IMAGES
 //   WF_DIAG_GUARD   N > 0: the trace kernel's block-queue claim gives up after N
 //                   iterations instead of 1024, so waves quit with rays unclaimed --
 //                   WRONG IMAGES; exercises the fault report (PNRT_E_TRACE)
@@ -31,10 +35,13 @@
 #ifndef WF_DIAG_VALU
 #define WF_DIAG_VALU 0
 #endif
+#ifndef WF_KO_STATE
+#define WF_KO_STATE 0
+#endif
 #ifndef WF_DIAG_GUARD
 #define WF_DIAG_GUARD 0
 #endif
-#if (WF_KO_ATTR || WF_KO_ENV || WF_DIAG_NOSTORE || WF_DIAG_GUARD) && !defined(PNRT_DIAG_BUILD)
+#if (WF_KO_ATTR || WF_KO_ENV || WF_KO_STATE || WF_DIAG_NOSTORE || WF_DIAG_GUARD) && !defined(PNRT_DIAG_BUILD)
 #error "result-changing knockout switches need -DPNRT_DIAG_BUILD (measurement builds only)"
 #endif
-#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_KO_ATTR || WF_KO_ENV || WF_DIAG_NOSTORE || WF_DIAG_VALU || WF_DIAG_GUARD)
+#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_KO_ATTR || WF_KO_ENV || WF_KO_STATE || WF_DIAG_NOSTORE || WF_DIAG_VALU || WF_DIAG_GUARD)

@@ -357,7 +357,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     // stored as soon as final (shorter live ranges), and only when shade can use it:
     // shade takes (0, 0) for a path without a light ray, as the reference's
     // initial LDirect / lightPDF (:878-879)
-    if (nfl & WF_RLIGHT) ps_st(w.P3, i, make_float4(LD.x, LD.y, LD.z, pl));
+    if ((nfl & WF_RLIGHT) && !WF_KO_STATE) ps_st(w.P3, i, make_float4(LD.x, LD.y, LD.z, pl));
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -373,7 +373,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
-    if (nfl & WF_RENV) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
+    if ((nfl & WF_RENV) && !WF_KO_STATE) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -432,8 +432,12 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
                           ((uint32_t)bounce << WF_META_BSHIFT);
     ps_st(w.P0, i, make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF));
     ps_st(w.P1, i, make_float4(L.x, L.y, L.z, NdotL));
-    ps_st(w.P2, i, make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe));
-    ps_st(w.P5, i, make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed)));
+    if (!WF_KO_STATE) {
+        ps_st(w.P2, i, make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe));
+        ps_st(w.P5, i, make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed)));
+    } else {     // knockout: keep the values live (no dead-code elimination of their math)
+        if (__float_as_uint(dBRDF.x + pe + q.Lo.x + LD.x + LE.x + pl) == 0x7fc00001u + seed) w.P2[i] = make_float4(0, 0, 0, 0);
+    }
     ps_st(w.P6, i, make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(meta)));
     return nfl | WF_RCONT;
 }
@@ -1085,8 +1089,9 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
                           float4* colors, uint32_t i, PathIn& q, int& bounce, uint32_t& slot, int& x, int& py,
                           uint32_t& frame) {
     const PathSet& rd = b.rd;
-    const float4 p0 = ps_ld(rd.P0 + i), p1 = ps_ld(rd.P1 + i), p2 = ps_ld(rd.P2 + i), p5 = ps_ld(rd.P5 + i),
-                 p6 = ps_ld(rd.P6 + i);
+    const float4 p0 = ps_ld(rd.P0 + i), p1 = ps_ld(rd.P1 + i), p6 = ps_ld(rd.P6 + i);
+    const float4 p2 = WF_KO_STATE ? make_float4(0.5f, 0.45f, 0.4f, 0.05f) : ps_ld(rd.P2 + i);
+    const float4 p5 = WF_KO_STATE ? make_float4(0.f, 0.f, 0.f, __uint_as_float(i * 0x9E3779B1u | 1u)) : ps_ld(rd.P5 + i);
     const int ht = b.hit[i];
     // the light / env candidates are read only where they count: an occluded
     // light ray zeroes LDirect and lightPDF (:890), an occluded or absent env ray
@@ -1099,8 +1104,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     slot = meta & WF_META_SLOT;
     const bool useL = (meta & WF_META_RL) && !(oc & 0xffu);
     const bool useE = (meta & WF_META_RE) && !(oc >> 8);
-    const float4 p3 = ps_ld(useL ? rd.P3 + i : s.zero4);
-    const float4 p4 = ps_ld(useE ? rd.P4 + i : s.zero4);
+    const float4 p3 = WF_KO_STATE ? make_float4(0.01f, 0.01f, 0.01f, 0.2f) : ps_ld(useL ? rd.P3 + i : s.zero4);
+    const float4 p4 = WF_KO_STATE ? make_float4(0.01f, 0.01f, 0.01f, 0.f) : ps_ld(useE ? rd.P4 + i : s.zero4);
     // the continuation hit's records, in flight while the MIS sum waits for P3/P4
     // (a miss reads triangle 0's, unused; so does an index a faulted trace left
     // stale -- reported as PNRT_E_TRACE, never a wild read)
