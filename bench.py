@@ -53,11 +53,18 @@ sys.path.insert(0, REPO)
 BAND = 8
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 (8 XCDs) ~34.5 TB/s
-# FETCH_SIZE (KiB) -> fabric read bytes.  MI355X_MICROARCH.md: gfx950's FETCH_SIZE counts
-# half the bytes of wide coalesced reads; the factor for the trace kernel's scattered 64-B
-# gathers is calibrated by tools/microtests/gather_pmc (profiles/r03/fetch_calibration.json)
-FETCH_FACTOR = 2.0
-FETCH_FACTOR_SOURCE = "MI355X_MICROARCH.md; 64-B gather calibration in profiles/r03/fetch_calibration.json"
+# FETCH_SIZE (KiB) -> fabric read bytes, calibrated on known byte counts over a 1 GiB table
+# (tools/microtests/fetch_calib.hip, tools/fetch_calib.py -> profiles/r03/fetch_calibration.json):
+# wide coalesced streaming reads (16 B per lane) are tallied at HALF their bytes (known /
+# FETCH_SIZE = 2.00, 128 B per TCC_EA0_RDREQ; MI355X_MICROARCH.md says the same), scattered
+# 64-B record gathers EXACTLY (0.994, 64 B per request; one 64-B half of each 128-B line:
+# 0.993).  The trace kernel mixes both: its ray records (origin + direction, 32 B per ray,
+# read once, streamed) and its node / triangle gathers (64-B requests).  So its fabric read
+# bytes = FETCH_SIZE + the streamed ray bytes / 2 (they were tallied at half), the ray count
+# from the census of these sources; the other kernels (path-state streams + gathers) are
+# reported at 2 x FETCH_SIZE, an upper bound.
+STREAM_FACTOR, GATHER_FACTOR = 2.0, 1.0
+CALIBRATION = "profiles/r03/fetch_calibration.json"
 # rocprofv3 --pmc passes (one run each; TCC block: FETCH_SIZE uses 3 counters, WRITE_SIZE 2)
 PMC_PASSES = [("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum")]
 KSHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
@@ -188,7 +195,8 @@ def live_pmc(args):
     for k, cs in counters.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
-        e = {"bytes_per_launch": (FETCH_FACTOR * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0,
+        e = {"bytes_per_launch": (STREAM_FACTOR * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024.0,
+             "fetch_bytes": cs["FETCH_SIZE"] * 1024.0, "write_bytes": cs["WRITE_SIZE"] * 1024.0,
              "launches_per_step": cs["_n"] / (steps + warm)}
         if "TCC_HIT_sum" in cs:
             e["l2_hit_rate"] = cs["TCC_HIT_sum"] / max(cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"], 1.0)
@@ -525,14 +533,32 @@ def main():
         traffic = l2hit = None
         traffic_src = None
         step_traffic = None
+        census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
+        census_scale = (rows0 / census.get("rows", H) * spp * ipc / census.get("frames", 4)) if census else None
+        traffic_bounds = None
         if pmc and kname in pmc:
-            traffic, l2hit = pmc[kname]["bytes_per_launch"], pmc[kname].get("l2_hit_rate")
-            traffic_src = (f"live rocprofv3 --pmc (FETCH_SIZE; WRITE_SIZE + TCC_HIT/MISS), {FETCH_FACTOR:g} x FETCH_SIZE "
-                           f"+ WRITE_SIZE ({FETCH_FACTOR_SOURCE})")
+            e = pmc[kname]
+            l2hit = e.get("l2_hit_rate")
+            traffic_bounds = [round(GATHER_FACTOR * e["fetch_bytes"] + e["write_bytes"]),
+                              round(STREAM_FACTOR * e["fetch_bytes"] + e["write_bytes"])]
+            if census and args.kernel == "v3":
+                # the launch's streamed ray records: 32 B per ray (census rays, scaled to the launch)
+                rays = sum(b["rays"] for b in census["per_bounce"]) / census["trace_launches"] * census_scale
+                streamed = min(32.0 * rays, e["fetch_bytes"] * STREAM_FACTOR)
+                traffic = e["fetch_bytes"] * GATHER_FACTOR + streamed / 2.0 + e["write_bytes"]
+                traffic_src = (f"live rocprofv3 --pmc: FETCH_SIZE + streamed ray bytes / 2 + WRITE_SIZE -- 64-B gathers "
+                               f"tallied exactly, streamed reads at half ({CALIBRATION}); {rays / 1e6:.1f}M rays x 32 B "
+                               f"per launch from profiles/census.json")
+            else:
+                traffic = traffic_bounds[0]
+                traffic_src = (f"live rocprofv3 --pmc: FETCH_SIZE + WRITE_SIZE, every read tallied as a 64-B gather "
+                               f"(lower bound; no census for these sources; {CALIBRATION})")
             step_traffic = {k: {"bytes_per_launch": round(e["bytes_per_launch"]),
                                 "launches_per_step": round(e["launches_per_step"], 3),
                                 "l2_hit_rate": round(e["l2_hit_rate"], 4) if "l2_hit_rate" in e else None}
                             for k, e in pmc.items()}
+            step_traffic["counting"] = (f"{STREAM_FACTOR:g} x FETCH_SIZE + WRITE_SIZE per launch: exact for the "
+                                        f"streamed path state, an upper bound for gathers ({CALIBRATION})")
             step_traffic["total_bytes_per_step"] = round(sum(e["bytes_per_launch"] * e["launches_per_step"]
                                                              for e in pmc.values()))
         else:
@@ -547,11 +573,9 @@ def main():
                                f"{e['bytes_per_launch']:.4g} B per {e['frames_per_launch']}-frame launch of "
                                f"{e['rows']} rows) x this rank's share ({rows0} rows, {spp * ipc} frames)")
         achieved = traffic / (kern_ms * 1e-3) / 1e9 if (traffic and kern_ms) else None
-        census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
         requested = None
         if census and kern_ms:
-            rb = (census["requested_bytes_per_launch"] * rows0 / census.get("rows", H)
-                  * spp * ipc / census.get("frames", 4))        # the census traced 4-frame calls
+            rb = census["requested_bytes_per_launch"] * census_scale      # the census traced 4-frame calls
             requested = {"bytes_per_launch": round(rb), "achieved": round(rb / (kern_ms * 1e-3) / 1e9, 1),
                          "peak": L2_PEAK_GBS, "unit": "GB/s",
                          "frac_of_l2": round(rb / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
@@ -587,6 +611,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
+                         "traffic_bounds": traffic_bounds,
                          "l2_hit_rate": round(l2hit, 4) if l2hit is not None else None,
                          "kernel": kfull, "kernel_ms": kern_ms, "kernel_ms_timing": "exclusive (PNRT_SERIAL steps)",
                          "kernel_ms_pipelined": round(kern_ms_pipe, 4) if kern_ms_pipe else None,

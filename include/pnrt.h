@@ -67,7 +67,11 @@ const char* pnrt_version(void);
 int pnrt_create(int device, pnrt_ctx** out);
 void pnrt_destroy(pnrt_ctx* ctx);
 const char* pnrt_last_error(pnrt_ctx* ctx);
-/* Launch work on `hip_stream` (a hipStream_t; NULL = the context's stream). */
+/* Launch work on `hip_stream` (a hipStream_t; NULL = the context's stream).
+ * The new stream is ordered after the last operation the context queued on the
+ * previous one (an event the context records with every such operation), so
+ * frame-ordered blends never overtake each other; the previous stream itself
+ * is not touched again and may already be destroyed. */
 int pnrt_set_stream(pnrt_ctx* ctx, void* hip_stream);
 /* The context's own stream (created with it, before its worker streams): a caller
  * that wraps it (e.g. torch.cuda.ExternalStream) adds no stream of its own. */

@@ -114,7 +114,9 @@ struct pnrt_ctx {
     };
     Pipe pipe[WF_PIPES];
     unsigned n_pipes_small = WF_PIPES;     // pipes small calls rotate over (pipes_init)
-    hipEvent_t ev_switch = nullptr;        // orders a pnrt_set_stream switch after the old stream's work
+    hipEvent_t ev_last = nullptr;          // recorded after every op the context queues on `stream`, so a
+    bool last_valid = false;               // pnrt_set_stream orders the new stream after it without
+                                           // touching the old stream (which the caller may have destroyed)
     bool pipes_ready = false;
     uint64_t ncall = 0;
     unsigned next_pipe = 0;
@@ -158,6 +160,14 @@ static int check_fault(pnrt_ctx* c) {
         if (e_ != hipSuccess)                                                                     \
             return set_err(ctx, PNRT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
     } while (0)
+
+// Record ev_last after an op queued on c->stream (see pnrt_set_stream).
+static int mark_stream(pnrt_ctx* c) {
+    HIPCHK(c, c->ev_last ? hipSuccess : hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_last, c->stream));
+    c->last_valid = true;
+    return PNRT_OK;
+}
 
 // every stream the context launches on (user-visible stream, blend stream, workers)
 static hipError_t sync_all(pnrt_ctx* c) {
@@ -251,6 +261,9 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #ifndef WF_TRACE_PATHS_PER_BLOCK
 #define WF_TRACE_PATHS_PER_BLOCK (8 * WF_TRACE_BLOCK) // > 0: trace grid <= paths / this (small multi-GPU shares)
 #endif
+#ifndef WF_TRACE_PATHS_PER_BLOCK_ALONE
+#define WF_TRACE_PATHS_PER_BLOCK_ALONE WF_TRACE_BLOCK  // ... for a call with no other call in flight
+#endif
 
 // Wavefront buffers of one batch of n path slots, carved from `base`.
 static size_t wf_bytes(size_t n) {
@@ -300,19 +313,21 @@ static WfLayout wf_layout(char* base, size_t n) {
 // Trace grid for a batch of n paths: small batches (a rank's share of a
 // multi-GPU frame) take a proportional part of the chip, and no launch more than
 // WF_TRACE_GRID_PCT % (WF_TRACE_GRID_PCT_LARGE % for large batches), so the calls
-// in flight trace side by side instead of queueing.
-static unsigned trace_grid_for(const pnrt_ctx* c, size_t n) {
-    const unsigned pct = c->serial ? 100u : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
+// in flight trace side by side instead of queueing.  A call submitted while no
+// other call is in flight (`alone`: an interactive loop that waits for every
+// frame, the reference's own 512x512 one-frame dispatch) has the chip to itself:
+// full occupancy, one block per WF_TRACE_PATHS_PER_BLOCK_ALONE paths.
+static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false) {
+    const unsigned pct = (c->serial || alone) ? 100u : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
     const size_t gmax = (size_t)c->trace_grid * pct / 100;
-    return WF_TRACE_PATHS_PER_BLOCK
-               ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + WF_TRACE_PATHS_PER_BLOCK - 1) / WF_TRACE_PATHS_PER_BLOCK))
-               : (unsigned)gmax;
+    const size_t ppb = alone ? WF_TRACE_PATHS_PER_BLOCK_ALONE : WF_TRACE_PATHS_PER_BLOCK;
+    return ppb ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + ppb - 1) / ppb)) : (unsigned)gmax;
 }
 
 // One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
 // its colours land in frame slots [0, cf) of `colors`.
 static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, const WfLayout& L, hipStream_t st,
-                        const float4* primary, float4* colors) {
+                        const float4* primary, float4* colors, bool alone) {
     WfBufs b = L.b;
     if (b.n > WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: too many paths per batch");
     const dim3 g((unsigned)((b.n + 255) / 256));
@@ -328,12 +343,12 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
-            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(trace_grid_for(c, b.n)), dim3(WF_TRACE_BLOCK), 0, st, s, b,
-                               fp.mode);
+            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(trace_grid_for(c, b.n, alone)), dim3(WF_TRACE_BLOCK), 0,
+                               st, s, b, fp.mode);
         }
         HIPCHK(c, hipGetLastError());
         if (WF_TIMING) {   // tail census: when the queue ran dry vs when the last wave ended
-            const size_t nw = (size_t)trace_grid_for(c, b.n) * (WF_TRACE_BLOCK / 64);   // waves launched
+            const size_t nw = (size_t)trace_grid_for(c, b.n, alone) * (WF_TRACE_BLOCK / 64);   // waves launched
             std::vector<unsigned long long> t(4 * nw);
             HIPCHK(c, hipStreamSynchronize(st));
             HIPCHK(c, hipMemcpy(t.data(), b.stats + 8, t.size() * 8, hipMemcpyDeviceToHost));
@@ -425,10 +440,12 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     if (per_frame > (size_t)WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: frame too large for one batch");
     const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
     const uint32_t chunk = nf < fit ? nf : fit;
-    // calls in flight by call size: small (multi-GPU shares) 4 with > 4 hardware queues;
-    // 1080p-class calls 2 -- their launches are long enough to fill each other's
-    // drains (C2 +1.8 %, C3 +2.7 %, C4 +1.6 % against 3); 4K-class calls 3, which
-    // hide more of their HBM-latency-bound traversal (C5 -3.5 % with 2)
+    // calls in flight by call size (paths per batch): small (< 5M: multi-GPU shares)
+    // 4 with > 4 hardware queues; 5M-32M (1080p calls of up to 15 frames) 2 -- their
+    // launches are long enough to fill each other's drains (8-frame calls: C2 +1.8 %,
+    // C3 +2.7 %, C4 +1.6 % against 3); above 32M 3: 4K calls, which hide more of their
+    // HBM-latency-bound traversal (C5 -3.5 % with 2), and the bench's 16-frame 1080p
+    // calls (33.2M paths), for which 2 and 3 measured the same within 1 %
     const size_t call_paths = per_frame * chunk;
     const unsigned want = c->serial ? 1u
                         : call_paths < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small
@@ -436,6 +453,10 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     const unsigned npipes = std::max(1u, std::min(want, c->n_pipes_small));   // only sets pipes_init made
     const unsigned pi = c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;
+    // no other call in flight: every pipe's last blend (its last work) has completed
+    bool alone = !c->serial;
+    for (auto& Q : c->pipe)
+        if (alone && Q.blend_pending && hipEventQuery(Q.ev_blend) != hipSuccess) alone = false;
     pnrt_ctx::Pipe& P = c->pipe[pi];
     if (c->trace_grid == 0) {
         int per_cu = 0, cus = 0;
@@ -499,11 +520,11 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
             bb.b.chunk_frames = (int)cfB;
             bb.b.tiles_x = tiles_x;
             bb.b.first_frame = first + f0 + cfA;
-            if ((rc = render_batch(c, s, fp, bb, w1, P.primary, P.colors + (size_t)cfA * pix))) return rc;
+            if ((rc = render_batch(c, s, fp, bb, w1, P.primary, P.colors + (size_t)cfA * pix, alone))) return rc;
             HIPCHK(c, hipEventRecord(P.ev_join[1], w1));
             HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[1], 0));
         }
-        if ((rc = render_batch(c, s, fp, a, w0, P.primary, P.colors))) return rc;
+        if ((rc = render_batch(c, s, fp, a, w0, P.primary, P.colors, alone))) return rc;
         HIPCHK(c, hipEventRecord(P.ev_join[0], w0));
         HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[0], 0));
         {   // the blends run in call order on the caller's stream
@@ -514,6 +535,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(P.ev_blend, c->stream));
         P.blend_pending = true;
+        if ((rc = mark_stream(c))) return rc;
     }
     return PNRT_OK;
 }
@@ -601,7 +623,7 @@ void pnrt_destroy(pnrt_ctx* c) {
 
     for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
+    if (c->ev_last) (void)hipEventDestroy(c->ev_last);
     if (c->fault_host) (void)hipHostFree(c->fault_host);
     (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -616,12 +638,12 @@ int pnrt_set_stream(pnrt_ctx* c, void* s) {
     hipStream_t ns = s ? static_cast<hipStream_t>(s) : c->own_stream;
     if (ns == c->stream) return PNRT_OK;
     // blends (frame-ordered read-modify-writes of accum), pack_rows and
-    // read_accum run on c->stream: the new stream starts after everything the
-    // old one holds, so no blend of a later call overtakes a pending one
+    // read_accum run on c->stream: the new stream starts after the last op the
+    // context queued on the old one (ev_last, recorded with it), so no blend of
+    // a later call overtakes a pending one -- and the old stream itself is not
+    // touched (the caller may have destroyed it since)
     HIPCHK(c, hipSetDevice(c->device));
-    if (!c->ev_switch) HIPCHK(c, hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming));
-    HIPCHK(c, hipEventRecord(c->ev_switch, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(ns, c->ev_switch, 0));
+    if (c->last_valid) HIPCHK(c, hipStreamWaitEvent(ns, c->ev_last, 0));
     c->stream = ns;
     return PNRT_OK;
 }
@@ -972,6 +994,7 @@ int pnrt_set_frame(pnrt_ctx* c, int w, int h, const pnrt_camera* cam, int depth)
         HIPCHK(c, hipMalloc(&c->accum, (size_t)w * h * 16));
         HIPCHK(c, hipMemsetAsync(c->accum, 0, (size_t)w * h * 16, c->stream));
         c->width = w; c->height = h;
+        if (int rc = mark_stream(c)) return rc;
     }
     c->cam = *cam;
     c->max_bounce = depth;
@@ -1037,7 +1060,7 @@ int pnrt_reset_accum(pnrt_ctx* c) {
     }
     if (!c->accum) return PNRT_OK;
     HIPCHK(c, hipMemsetAsync(c->accum, 0, (size_t)c->width * c->height * 16, c->stream));
-    return PNRT_OK;
+    return mark_stream(c);
 }
 
 int pnrt_read_accum(pnrt_ctx* c, float* out) {
@@ -1087,7 +1110,7 @@ int pnrt_pack_rows(pnrt_ctx* c, void* dst, int band, int nsh, int shard) {
     hipLaunchKernelGGL(pt_pack_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream,
                        c->accum, static_cast<float4*>(dst), c->width, rows, band, nsh, shard);
     HIPCHK(c, hipGetLastError());
-    return PNRT_OK;
+    return mark_stream(c);
 }
 
 int pnrt_synchronize(pnrt_ctx* c) {

@@ -172,8 +172,11 @@ def write_obj(path: str, meshes, material_names=None, mtllib: str | None = None)
     """Write meshes as a Wavefront OBJ that :func:`load_obj` reads back to the
     same triangles: one ``o``/``usemtl`` per mesh, positions and normals as
     ``%.9g`` (float32 round-trips exactly), texcoords stored pre-flipped
-    (``vt u 1-v``) for FlipUVs, faces in index order.  (Scene export for tests
-    and tools; the reference only reads OBJ.)"""
+    (``vt u 1-v``) for FlipUVs, faces in index order.  u round-trips exactly;
+    v comes back as float32 ``1 - (1 - v)``, within 2^-24 of v (exact for v in
+    [0.5, 1] and for multiples of 2^-24), since FlipUVs on the read side cannot
+    be undone bit for bit for every v.  (Scene export for tests and tools; the
+    reference only reads OBJ.)"""
     with open(path, "w", encoding="utf-8") as f:
         if mtllib:
             f.write(f"mtllib {mtllib}\n")

@@ -3,6 +3,8 @@ configs[1..4]), against the CPU oracle and through size-independent
 properties.
 
 * C2 (1920x1080, 4 spp, the bench frame): every pixel vs the oracle.
+* C3 (1920x1080, textured figure + metal boards + env: albedo textures,
+  every Disney lobe): every pixel vs the oracle.
 * C4 (1920x1080, teapot + area light + env: all three pdfs active): every
   pixel vs the oracle.
 * C5 (3840x2160, 4.19M triangles, 4k env): every 16th row vs the oracle.
@@ -64,6 +66,17 @@ def test_c2_whole_frame_bitwise(pt):
     ref, st = pyoracle.Oracle(c).render(0, 4)
     assert st["stack_overflow"] == 0
     assert_bitwise(got, ref, "C2 1920x1080 whole frame")
+
+
+def test_c3_whole_frame_bitwise(pt):
+    """C3 at its full 1920x1080 x 4 spp, every pixel: albedo textures (RGBA
+    2048x1024 and an odd-width RGB one, GL unpack alignment), every Disney
+    lobe, the env (it was checked on every 45th row only)."""
+    c = cfg("C3")
+    got = gpu_render(pt, c, 0, 4)
+    ref, st = pyoracle.Oracle(c).render(0, 4)
+    assert st["albedo_bytes"] > 0 and st["env_samples"] > 0 and st["stack_overflow"] == 0
+    assert_bitwise(got, ref, "C3 1920x1080 whole frame")
 
 
 def test_c4_whole_frame_bitwise(pt):

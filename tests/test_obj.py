@@ -134,3 +134,26 @@ def test_obj_round_trip_same_triangles_and_bvh(tmp_path):
     for k in range(3):       # corner k of every triangle: same position and normal (cols 0-5)
         pa, pb = va[ta[:, k].astype(np.int64), :6], vb[tb[:, k].astype(np.int64), :6]
         assert np.array_equal(pa.view(np.uint32), pb.view(np.uint32))
+
+
+def test_obj_round_trip_texcoords(tmp_path):
+    """write_obj -> load_obj on a mesh with non-trivial texcoords: positions,
+    normals and u exactly; v (flipped by FlipUVs on the way in and back) within
+    2^-24, exactly for v in [0.5, 1]."""
+    rng = np.random.default_rng(5)
+    m = H.mesh_displaced_sphere(12, 8, 1.0, (0.0, 0.0, 0.0), 0.05, 7)
+    uv = rng.random((len(m.positions), 2)).astype(np.float32)
+    uv[:4] = [[0.0, 0.0], [1.0, 1.0], [0.1, 0.5], [0.75, 1e-9]]
+    m = H.Mesh(m.positions, m.normals, uv, m.indices)
+    p = str(tmp_path / "uv.obj")
+    obj.write_obj(p, [m])
+    back = obj.load_obj(p)[0].mesh
+    idx = np.asarray(m.indices, np.int64)
+    got = np.asarray(back.texcoords, np.float32)          # one vertex per face corner, in face order
+    want = uv[idx]
+    assert np.array_equal(got[:, 0].view(np.uint32), want[:, 0].view(np.uint32))
+    assert np.max(np.abs(got[:, 1].astype(np.float64) - want[:, 1])) <= 2.0 ** -24
+    hi = want[:, 1] >= 0.5
+    assert np.array_equal(got[hi, 1].view(np.uint32), want[hi, 1].view(np.uint32))
+    assert np.array_equal(np.asarray(back.positions, np.float32).view(np.uint32),
+                          np.asarray(m.positions, np.float32)[idx].view(np.uint32))
