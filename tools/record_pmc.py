@@ -21,7 +21,7 @@ def main(paths):
         old = json.load(open(OUT))
         db = {k: v for k, v in old.items() if "source_hash" in v}      # drop entries without a source hash
     for p in paths:
-        line = json.loads(open(p).read().strip().splitlines()[-1])
+        line = [json.loads(x) for x in open(p) if x.startswith("{")][-1]
         r, c = line["roofline"], line["config"]
         if line["n_gpus"] != 1 or not r.get("traffic"):
             print(f"{p}: not an N = 1 line with live traffic; skipped")
