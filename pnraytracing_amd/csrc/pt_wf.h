@@ -512,24 +512,10 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
 #define WF_GEN_WAVES WF_SHADE_WAVES   // waves per SIMD for the gen/setup kernel
 #endif
 
-#ifndef WF_GEN_XCD
-#define WF_GEN_XCD 0        // 1: gen's path slots dealt to blocks XCD-aware (see xcd_block)
-#endif
-// Workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b % 8),
-// each with its own L2.  xcd_block gives the blocks of one XCD a contiguous run
-// of logical blocks, so the consecutive blocks that share data (gen: the 4 blocks
-// of an 8x8-pixel tile read the same 64 primary records) share an L2.  A
-// bijection on the first n & ~7 blocks; the rest keep their index.
-PN_DEV uint32_t xcd_block(uint32_t blk, uint32_t n) {
-    const uint32_t full = n & ~7u;
-    return blk >= full ? blk : (blk & 7u) * (full >> 3) + (blk >> 3);
-}
-
 // ---- gen + bounce-0 setup: start every path from its pixel's primary hit -------------------
 __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s, FrameParams fp, WfBufs b, const float4* primary,
                                                        float4* colors) {
-    // path slot (its block XCD-aware with WF_GEN_XCD; the compacted outputs stay by blockIdx)
-    const uint32_t i = (WF_GEN_XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     // path slot
     wf_reset_counters(b);
     bool cont = false;
     PathIn q;
@@ -661,20 +647,11 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
-#ifndef WF_LT_BYTES
-#define WF_LT_BYTES 0       // 1: a lane's pending triangle (and its accepted one) as the record's byte
-#endif                      // offset in the geometry buffer, not its index (no multiply per step)
-// triangle index -> the lane's triangle position (index, or byte offset with WF_LT_BYTES)
-PN_DEV int wf_tri_pos(const DevScene& s, int i) { return WF_LT_BYTES ? (int)(s.geo_tri_off + (uint32_t)i * 48u) : i; }
-PN_DEV int wf_tri_index(const DevScene& s, int pos) {
-    return WF_LT_BYTES ? (int)(((uint32_t)pos - s.geo_tri_off) / 48u) : pos;
-}
-
 // One lane's traversal state (a ray being traced).
 struct TravState {
     RayP r;
     float tMax;
-    int hitTri, lt, lc;       // accepted triangle; pending triangle range [lt, lt + lc) (wf_tri_pos)
+    int hitTri, lt, lc;       // accepted triangle; pending triangle range [lt, lt + lc)
     uint32_t spa, cur;        // stack position (see wf_push); node to visit next
     bool any;                 // any-hit (shadow) ray
     uint32_t nst;             // WF_STATS builds: lane steps of this ray
@@ -699,8 +676,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool isNode = !isTri & (t.cur != REF_NONE);
     // ---- the step's single fetch: a triangle record or a node (lanes
     // with neither re-read node 0, which stays in L1)
-    const uint32_t off = isTri ? (WF_LT_BYTES ? (uint32_t)t.lt : s.geo_tri_off + (uint32_t)t.lt * 48u)
-                               : (isNode ? t.cur : 0u) * 64u;
+    const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)t.lt * 48u : (isNode ? t.cur : 0u) * 64u;
     // triangle lanes read the unused fourth quarter from one shared address
     // (one cache access per wave instead of one per lane)
     const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
@@ -713,7 +689,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     t.hitTri = acc ? t.lt : t.hitTri;
     bool done = acc & t.any;
     if (acc & !t.any) t.tMax = ts * (1.0f / det);
-    t.lt += isTri ? (WF_LT_BYTES ? 48 : 1) : 0;
+    t.lt += isTri ? 1 : 0;
     t.lc -= isTri ? 1 : 0;
     // node visit: both child boxes (:447-457), z-slab culling
     const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
@@ -737,7 +713,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
     int gs, gc;
     decode_leaf_fast(s, go, gs, gc);
-    t.lt = goLeaf ? wf_tri_pos(s, gs) : t.lt;
+    t.lt = goLeaf ? gs : t.lt;
     t.lc = goLeaf ? gc : t.lc;
     t.cur = isNode ? (goLeaf ? REF_NONE : go) : t.cur;
     // ---- next fetch target: pop when nothing is pending
@@ -750,7 +726,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
         int es, ec;
         decode_leaf_fast(s, e.x, es, ec);
-        t.lt = (!culled & eLeaf) ? wf_tri_pos(s, es) : t.lt;
+        t.lt = (!culled & eLeaf) ? es : t.lt;
         t.lc = (!culled & eLeaf) ? ec : t.lc;
         t.cur = (!culled & !eLeaf) ? e.x : t.cur;
     }
@@ -1008,8 +984,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (done) {
                 const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
                 if (!WF_DIAG_NOSTORE) {
-                    if (kind == 2) b.hit[p] = t.hitTri == -1 ? -1 : wf_tri_index(s, t.hitTri);
-                    else b.occ[2 * (size_t)p + kind] = t.hitTri != -1 ? 1 : 0;
+                    if (kind == 2) b.hit[p] = t.hitTri;
+                    else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
                 }
                 busy = 0;
             }
@@ -1057,7 +1033,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
                     t.r = nr; t.tMax = ntmax; t.any = nany; rid = (kind << 30) | p;
-                    t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = wf_tri_pos(s, nlt); t.lc = nlc;
+                    t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
                     t.nst = 0;
                     busy = 1;
                 }
