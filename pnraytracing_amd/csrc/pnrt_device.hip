@@ -490,7 +490,15 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     }
     {
         ProfScope ps(c, PNRT_K_PRIMARY, w0);
-        hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
+        if (PT_PRIM_WF) {     // the trace kernel's step, grid-stride, the call's first spill area
+            WfBufs pb{};
+            pb.ovf = P.ovf[0];
+            pb.ovf_stride = (uint32_t)ovf_stride;
+            const unsigned gp = (unsigned)std::min<size_t>((pix + WF_TRACE_BLOCK - 1) / WF_TRACE_BLOCK, (size_t)c->trace_grid);
+            hipLaunchKernelGGL((pt_primary_wf<WF_STACK>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w0, s, fp, pb, P.primary);
+        } else {
+            hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
+        }
     }
     HIPCHK(c, hipGetLastError());
     if (w1 != w0) {

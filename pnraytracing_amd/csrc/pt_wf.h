@@ -1095,6 +1095,77 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         for (int k = 0; k < 8; ++k) atomicAdd(b.stats + k, st[k]);
 }
 
+// ---- primary hits through the trace kernel's step (PT_PRIM_WF) --------------------------------
+// The primary pass (pt_passes.h pt_primary_kernel) with the branch-light unified
+// step of pt_wf_trace instead of its node / leaf loops: one camera ray per lane,
+// grid-stride over 256-pixel chunks (grid <= the trace grid, so the trace's stack
+// spill area serves it), the same visit order and culling, the same record.
+#ifndef PT_PRIM_WF
+#define PT_PRIM_WF 0
+#endif
+#ifndef PT_PRIM_WF_WAVES
+#define PT_PRIM_WF_WAVES 7
+#endif
+template <int STK>
+__global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_wf(DevScene s, FrameParams fp, WfBufs b,
+                                                                               float4* rec) {
+    __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
+    const __amdgpu_buffer_rsrc_t geo =
+        __builtin_amdgcn_make_buffer_rsrc((void*)s.nodes, (short)0, (int)s.geo_bytes, 0x00020000);
+    const size_t npix = (size_t)fp.rows * fp.width;
+    for (size_t base = (size_t)blockIdx.x * WF_TRACE_BLOCK; base < npix; base += (size_t)gridDim.x * WF_TRACE_BLOCK) {
+        const size_t i = base + threadIdx.x;
+        const bool mine = i < npix;
+        const int lr = mine ? (int)(i / fp.width) : 0, px = mine ? (int)(i - (size_t)lr * fp.width) : 0;
+        const int py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
+        const f3 eye = mk3(fp.eye[0], fp.eye[1], fp.eye[2]);
+        const f3 dir = camera_dir(fp, px, py);
+        TravState t;
+        t.r = make_ray(eye, dir, fp.mode);
+        t.tMax = PT_FLOAT_MAX;
+        t.hitTri = -1; t.lt = 0; t.lc = 0;
+        t.spa = (uint32_t)threadIdx.x * 8u;
+        t.cur = REF_NONE;
+        t.any = false;
+        float zlo;
+        if (mine && box_fast(t.r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
+                             s.root_max[2], zlo)) {
+            t.cur = s.root_ref;
+            if (t.cur & REF_LEAF) { decode_leaf(s, t.cur, t.lt, t.lc); t.cur = REF_NONE; }
+        }
+        int busy = mine && (t.cur != REF_NONE || t.lc > 0);
+        auto run = [&](auto ident_tag) {
+            constexpr bool ID = decltype(ident_tag)::value;
+            for (;;) {
+                const uint32_t need = WF_SKIP_HALF ? (__ballot(busy != 0 && t.lc > 0) != 0 ? 1u : 0u) |
+                                                         (__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE) != 0 ? 2u : 0u)
+                                                   : 3u;
+                if (busy && wf_step<STK, ID>(s, b, geo, lds, t, need)) busy = 0;
+                if (__ballot(busy != 0) == 0) break;
+            }
+        };
+        if (__ballot(busy != 0 && t.r.kz() != 2) == 0) run(std::true_type{});
+        else run(std::false_type{});
+        if (!mine) continue;
+        float4 q0, q1, q2;
+        if (t.hitTri >= 0) {
+            Hit h = make_hit(s, t.r, t.hitTri);
+            f3 em = get_emissive(s, h.mat);
+            q0 = make_float4(h.P.x, h.P.y, h.P.z, __int_as_float((h.mat & 0x00ffffff) | ((h.tex + 1) << 24)));
+            q1 = make_float4(h.N.x, h.N.y, h.N.z, h.u);
+            q2 = make_float4(h.v, em.x, em.y, em.z);
+        } else {
+            f3 c = env_color(s, dir);
+            q0 = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+            q1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            q2 = make_float4(0.f, c.x, c.y, c.z);
+        }
+        rec[3 * i] = q0;
+        rec[3 * i + 1] = q1;
+        rec[3 * i + 2] = q2;
+    }
+}
+
 // ---- shade: MIS, continuation hit, next bounce or final colour (:936-972) --------------------
 // Path entry i of the read set.  Returns whether the path continues; then q,
 // bounce, slot and the pixel / frame carry its next bounce to the setup.
