@@ -657,16 +657,11 @@ struct TravState {
     uint32_t nst;             // WF_STATS builds: lane steps of this ray
 };
 
-#ifndef WF_SKIP_HALF
-#define WF_SKIP_HALF 0      // 1: skip the triangle test / the node visit when no lane of the wave needs it
-#endif                      //    (wave-uniform, decided at the step's reconvergence point: `need`)
 // One traversal step of a lane's ray; returns true when the ray is finished
-// (an any-hit ray accepted a triangle, or nothing is left to visit).  need: bit 0 =
-// some lane of the wave tests a triangle this step, bit 1 = some lane visits a node
-// (wave-uniform; 3 = both, the common case in a full wave).
+// (an any-hit ray accepted a triangle, or nothing is left to visit).
 template <int STK, bool ID>
 PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo,
-                                                   uint2* lds, TravState& t, uint32_t need = 3u) {
+                                                   uint2* lds, TravState& t) {
     // One step, written branch-light: the triangle test and the node
     // visit are both evaluated (a wave almost always holds lanes of
     // both kinds, so both paths ran anyway) and their results are
@@ -683,9 +678,8 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
                  q3 = geo_load(geo, off3);
     // triangle test (:254-357 / :360-424)
-    float e0, e1, e2, det = 1.f, ts = 0.f;
-    bool acc = false;
-    if (need & 1u) acc = tri_test<ID>(t.r, q0, q1, q2, t.tMax, e0, e1, e2, det, ts) & isTri;
+    float e0, e1, e2, det, ts;
+    const bool acc = tri_test<ID>(t.r, q0, q1, q2, t.tMax, e0, e1, e2, det, ts) & isTri;
     t.hitTri = acc ? t.lt : t.hitTri;
     bool done = acc & t.any;
     if (acc & !t.any) t.tMax = ts * (1.0f / det);
@@ -695,15 +689,12 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
                                __float_as_uint(q3.w));
     const float tmc = t.tMax * 1.000001f;
-    float zloL = 0.f, zloR = 0.f;
-    bool hL = false, hR = false;
+    float zloL, zloR;
+    bool hL = box_fast<ID>(t.r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+    bool hR = box_fast<ID>(t.r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
     const bool cull = t.r.cull_ok();
-    if (need & 2u) {
-        hL = box_fast<ID>(t.r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
-        hR = box_fast<ID>(t.r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
-        hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
-        hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
-    }
+    hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
+    hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
     const bool rightFirst = comp(t.r.d, (int)(m.z & 3u)) < 0;     // :448
     const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
     const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
@@ -972,12 +963,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
         }
         if (WF_TIMING) ++witer;
-        // which halves of the step some lane needs (wave-uniform, at the reconvergence point)
-        const uint32_t need = WF_SKIP_HALF ? (__ballot(busy != 0 && t.lc > 0) != 0 ? 1u : 0u) |
-                                                 (__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE) != 0 ? 2u : 0u)
-                                           : 3u;
         if (busy) {
-            const bool done = wf_step<STK, ID>(s, b, geo, lds, t, need);
+            const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
             if (WF_STATS || WF_TIMING) t.nst += 1;
             if (WF_STATS && done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (rid >> 30) << 16 | min(t.nst, 0xffffu);
@@ -1101,7 +1088,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 // grid-stride over 256-pixel chunks (grid <= the trace grid, so the trace's stack
 // spill area serves it), the same visit order and culling, the same record.
 #ifndef PT_PRIM_WF
-#define PT_PRIM_WF 0
+#define PT_PRIM_WF 1        // 0: the one-lane-per-pixel loop pass of pt_passes.h (C2 neutral, D2 -4 %)
 #endif
 #ifndef PT_PRIM_WF_WAVES
 #define PT_PRIM_WF_WAVES 7
@@ -1137,10 +1124,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_w
         auto run = [&](auto ident_tag) {
             constexpr bool ID = decltype(ident_tag)::value;
             for (;;) {
-                const uint32_t need = WF_SKIP_HALF ? (__ballot(busy != 0 && t.lc > 0) != 0 ? 1u : 0u) |
-                                                         (__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE) != 0 ? 2u : 0u)
-                                                   : 3u;
-                if (busy && wf_step<STK, ID>(s, b, geo, lds, t, need)) busy = 0;
+                if (busy && wf_step<STK, ID>(s, b, geo, lds, t)) busy = 0;
                 if (__ballot(busy != 0) == 0) break;
             }
         };
