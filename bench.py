@@ -68,7 +68,7 @@ CALIBRATION = "profiles/r03/fetch_calibration.json"
 # rocprofv3 --pmc passes (one run each; TCC block: FETCH_SIZE uses 3 counters, WRITE_SIZE 2)
 PMC_PASSES = [("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum")]
 KSHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
-          "pt_primary_kernel": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
+          "pt_primary_kernel": "primary", "pt_primary_wf": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
 
 
 def parse():

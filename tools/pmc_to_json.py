@@ -12,7 +12,7 @@ rows = int(sys.argv[2]) if len(sys.argv) > 2 else 1080
 root = os.environ.get("PMC_ROOT") or os.path.join(REPO, "gpurun_out", "pmc")
 SHORT = {"pt_wf_trace": "trace", "pt_wf_setup": "setup", "pt_wf_shade": "shade", "pt_wf_gen": "gen",
          "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
-         "pt_primary_kernel": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
+         "pt_primary_kernel": "primary", "pt_primary_wf": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*_default", "run_counter_collection.csv"))):
     per = collections.defaultdict(lambda: collections.defaultdict(float))

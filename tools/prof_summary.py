@@ -17,7 +17,7 @@ import statistics
 import sys
 
 SHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
-         "pt_primary_kernel": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
+         "pt_primary_kernel": "primary", "pt_primary_wf": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
 
 
 def main():

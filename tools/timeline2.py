@@ -6,7 +6,7 @@ alone / beside shade / beside gen.
 import csv
 import sys
 
-CLS = {"pt_wf_trace": "trace", "pt_wf_shade_setup": "shade", "pt_wf_gen_setup": "gen", "pt_primary_kernel": "primary",
+CLS = {"pt_wf_trace": "trace", "pt_wf_shade_setup": "shade", "pt_wf_gen_setup": "gen", "pt_primary_kernel": "primary", "pt_primary_wf": "primary",
        "pt_blend_kernel": "blend"}
 rows = []
 for r in csv.DictReader(open(sys.argv[1])):
