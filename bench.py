@@ -337,15 +337,17 @@ def launches_per_step_of(k_launches: int, steps: int, excl: dict, kname: str):
 
 
 def derive_bound(hbm_frac, l2_hit, l2_frac):
-    """The roof that binds, from the counters: HBM when the kernel's fabric
-    traffic is at least half the HBM peak, or when most L2 lookups miss and the
-    HBM fraction exceeds the L2 one; otherwise the kernel is bound by dependent
-    L1/L2-hit fetch latency."""
+    """The roof that binds, from the counters: "hbm" (bandwidth) when the kernel's
+    fabric traffic reaches half the HBM peak; below that the kernel is bound by
+    the latency of its dependent fetch chains -- "hbm-latency" when most of its L2
+    lookups miss (a scene beyond the L2s: C5), "l2-latency" when they hit (C2:
+    L1/L2-hit chains).  l2_frac (its own requests against
+    the L2 bandwidth) is reported beside it."""
     if hbm_frac is None:
         return None
-    if hbm_frac >= 0.5 or (l2_hit is not None and l2_hit < 0.6 and (l2_frac is None or hbm_frac >= l2_frac)):
+    if hbm_frac >= 0.5:
         return "hbm"
-    return "l2-latency"
+    return "hbm-latency" if (l2_hit is not None and l2_hit < 0.6) else "l2-latency"
 
 
 def main():
@@ -604,9 +606,9 @@ def main():
                        "kernel": kfull},
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
                                                requested["frac_of_l2"] if requested else None),
-                         "bound_rule": "derived from the counters (bench.derive_bound): hbm if frac >= 0.5, or "
-                                       "if l2_hit_rate < 0.6 and frac >= requested.frac_of_l2; else l2-latency "
-                                       "(dependent L1/L2-hit fetch chains); peak / frac stay against HBM",
+                         "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "
+                                       "else the latency of dependent fetch chains -- hbm-latency if l2_hit_rate < 0.6, "
+                                       "l2-latency otherwise; peak / frac stay against HBM",
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

@@ -52,8 +52,8 @@ def test_launch_count_without_kernel_events():
 
 def test_bound_derived_from_counters():
     b = _bench()
-    assert b.derive_bound(0.16, 0.80, 0.34) == "l2-latency"     # C2: L1/L2-hit chains
-    assert b.derive_bound(0.43, 0.52, 0.20) == "hbm"            # C5: 1 GB scene, half the L2 lookups miss
+    assert b.derive_bound(0.13, 0.80, 0.32) == "l2-latency"     # C2: L1/L2-hit chains
+    assert b.derive_bound(0.25, 0.52, 0.30) == "hbm-latency"    # C5: 1 GB scene, half the L2 lookups miss
     assert b.derive_bound(0.62, 0.90, 0.30) == "hbm"
     assert b.derive_bound(None, 0.5, 0.3) is None
 
