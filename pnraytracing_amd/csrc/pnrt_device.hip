@@ -468,8 +468,6 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
     const size_t ovf_bytes = (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8;
-    // + the tail-help result keys (WF_TAIL_HELP): one per trace lane slot, after the spill area
-    const size_t tail_bytes = WF_TAIL_HELP ? (size_t)c->trace_grid * WF_TRACE_BLOCK * 8 : 0;
     const uint32_t cfA0 = split ? (chunk + 1) / 2 : chunk;
     const size_t bytesA = wf_bytes(per_frame * cfA0), bytesB = split ? wf_bytes(per_frame * (chunk - cfA0)) : 0;
     // every buffer set this call size rotates over is sized now, so no later call of
@@ -479,8 +477,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         if ((rc = grow(c, (void**)&Q.primary, &Q.primary_cap, pix * 48)) ||
             (rc = grow(c, (void**)&Q.colors, &Q.colors_cap, pix * 16 * chunk)) ||
             (rc = grow(c, &Q.wf, &Q.wf_cap, bytesA + bytesB + 512)) ||
-            (rc = grow(c, (void**)&Q.ovf[0], &Q.ovf_cap[0], ovf_bytes + tail_bytes)) ||
-            (split && (rc = grow(c, (void**)&Q.ovf[1], &Q.ovf_cap[1], ovf_bytes + tail_bytes))))
+            (rc = grow(c, (void**)&Q.ovf[0], &Q.ovf_cap[0], ovf_bytes)) ||
+            (split && (rc = grow(c, (void**)&Q.ovf[1], &Q.ovf_cap[1], ovf_bytes))))
             return rc;
     }
     ++c->ncall;
@@ -513,7 +511,6 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         char* base = static_cast<char*>(P.wf);
         WfLayout a = wf_layout(base, per_frame * cfA);
         a.b.ovf = P.ovf[0];
-        a.b.tail_key = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(P.ovf[0]) + ovf_bytes);
         a.b.fault = c->fault_dev;
         a.b.ovf_stride = (uint32_t)ovf_stride;
         a.b.chunk_frames = (int)cfA;
@@ -526,7 +523,6 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         if (cfB) {
             WfLayout bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
             bb.b.ovf = P.ovf[1];
-            bb.b.tail_key = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(P.ovf[1]) + ovf_bytes);
             bb.b.fault = c->fault_dev;
             bb.b.ovf_stride = (uint32_t)ovf_stride;
             bb.b.chunk_frames = (int)cfB;

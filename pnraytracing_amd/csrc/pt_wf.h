@@ -154,7 +154,6 @@ struct WfBufs {
     uint32_t nseg_k;         // setup blocks = segments per kind
     unsigned long long* stats; // WF_STATS builds: traversal step census (8 counters)
     uint32_t* fault;   // the context's fault words (host-mapped, see wf_fault), WF_FAULT_* index
-    unsigned long long* tail_key;   // WF_TAIL_HELP: one result key per trace lane slot (grid x block)
     uint32_t n;        // path slots
     int chunk_frames;
     int tiles_x;
@@ -648,43 +647,6 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
-// ---- tail help (WF_TAIL_HELP) -------------------------------------------------------------
-// Once a wave's ray queue is exhausted, its idle lanes help the lanes still
-// tracing: a helper takes the BOTTOM entry of an owner's LDS stack (the subtree
-// the owner would visit last), which the owner finds replaced by an empty-leaf
-// sentinel, and traverses it with a copy of the owner's ray.  Exactness:
-// * any-hit rays: occlusion = OR over the parts (the reachable set of a fixed
-//   tMax does not depend on the visit order);
-// * closest-hit rays: the reference result is the accepted triangle of least t,
-//   ties to the LAST one in visit order (`>` rule).  Each part keeps its own
-//   tMax (>= the owner's at the steal, so it finds a superset of the triangles
-//   of least t in its subtree, in the reference's order within it); the parts
-//   combine by a 64-bit key (t bits, tie, triangle) under atomicMin, with tie =
-//   the stolen depth d for a helper (bottom = visited last = 0 wins) and 255 for
-//   the owner.  Stolen depths are taken bottom-up, so each new steal is visited
-//   before every earlier one -- until the owner pops a sentinel, i.e. reaches the
-//   stolen region, after which entries it pushes would come AFTER stolen ones:
-//   then it is never stolen from again.
-// Per owner slot: th_meta (LDS) = parts still running (bits 0-15) | next depth to
-// steal (bits 16-23; 0xFF = no more); per helper: th_link = owner slot | d << 8.
-#ifndef WF_TAIL_HELP
-#define WF_TAIL_HELP 0
-#endif
-#define WF_STOLEN 0xBFFFFF80u      // an empty leaf (count 0) no child ref equals: a stolen stack entry
-#define WF_RID_P 0x03ffffffu       // ray id = kind << 30 | flags | path entry
-#define WF_RID_SHARED (1u << 29)   // the ray is split into parts (owner or helper)
-#define WF_RID_HELPER (1u << 28)   // this lane traces a stolen part
-// index of the k-th (0-based) set bit of m (k < popcount(m))
-PN_DEV uint32_t kth_bit(uint64_t m, uint32_t k) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const uint32_t c = (uint32_t)__popcll((m >> pos) & ((1ull << w) - 1ull));
-        if (k >= c) { k -= c; pos += (uint32_t)w; }
-    }
-    return pos;
-}
-
 // One lane's traversal state (a ray being traced).
 struct TravState {
     RayP r;
@@ -699,7 +661,7 @@ struct TravState {
 // (an any-hit ray accepted a triangle, or nothing is left to visit).
 template <int STK, bool ID>
 PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo,
-                                                   uint2* lds, TravState& t, uint32_t* th_meta = nullptr) {
+                                                   uint2* lds, TravState& t) {
     // One step, written branch-light: the triangle test and the node
     // visit are both evaluated (a wave almost always holds lanes of
     // both kinds, so both paths ran anyway) and their results are
@@ -750,8 +712,6 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     done = done | (idle & (t.spa < WF_SPA_STRIDE));
     if (idle & (t.spa >= WF_SPA_STRIDE)) {
         const uint2 e = wf_pop<STK>(lds, b, t.spa);
-        // tail help: the owner reached a stolen entry -- never steal from it again
-        if (WF_TAIL_HELP && th_meta && e.x == WF_STOLEN) atomicOr(&th_meta[threadIdx.x], 0xFFu << 16);
         const float z = __uint_as_float(e.y);
         const bool culled = cull & (z > t.tMax * 1.000001f) & (z > 1e-20f);
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
@@ -836,13 +796,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     // current generation's segment is used up.  Per-wave queue: bk_cnt[0] = rays
     // dequeued - rays loaded.  bk_cnt[1] counts the waves that have left.
     __shared__ uint32_t bk_cnt[2];
-    __shared__ uint32_t th_meta[WF_TAIL_HELP ? WF_TRACE_BLOCK : 1];
-    __shared__ uint16_t th_link[WF_TAIL_HELP ? WF_TRACE_BLOCK : 1];
-    if (WF_TAIL_HELP) {
-        th_meta[threadIdx.x] = 0u;
-        th_link[threadIdx.x] = 0;
-        b.tail_key[(size_t)blockIdx.x * WF_TRACE_BLOCK + threadIdx.x] = ~0ull;
-    }
     if (!WF_BLOCKQ) {
         if (threadIdx.x == 0) bk_cnt[0] = bk_cnt[1] = 0u;
         __syncthreads();
@@ -1010,20 +963,18 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
         }
         if (WF_TIMING) ++witer;
-        if (WF_TAIL_HELP ? busy == 1 : busy != 0) {
-            const bool done = wf_step<STK, ID>(s, b, geo, lds, t, WF_TAIL_HELP ? th_meta : nullptr);
+        if (busy) {
+            const bool done = wf_step<STK, ID>(s, b, geo, lds, t);
             if (WF_STATS || WF_TIMING) t.nst += 1;
             if (WF_STATS && done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
-                const uint32_t kind = rid >> 30, p = rid & WF_RID_P;
+                const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
                 if (!WF_DIAG_NOSTORE) {
-                    if (!WF_TAIL_HELP || !(rid & WF_RID_SHARED)) {
-                        if (kind == 2) b.hit[p] = t.hitTri;
-                        else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
-                    }
+                    if (kind == 2) b.hit[p] = t.hitTri;
+                    else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
                 }
-                busy = (WF_TAIL_HELP && (rid & WF_RID_SHARED)) ? 2 : 0;   // a part of a split ray: combined below
+                busy = 0;
             }
         }
 #if WF_DIAG_VALU
@@ -1037,26 +988,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     };
 
     for (;;) {
-        if (WF_TAIL_HELP && __ballot(busy == 2) != 0 && busy == 2) {
-            // ---- tail help: a finished part of a split ray combines its result; the
-            // ray's last part stores it
-            const uint32_t kind = rid >> 30, p = rid & WF_RID_P;
-            const bool hlp = (rid & WF_RID_HELPER) != 0;
-            const uint32_t link = hlp ? th_link[threadIdx.x] : 0u;
-            const uint32_t o = hlp ? (link & 0xFFu) : threadIdx.x;
-            unsigned long long* key = b.tail_key + (size_t)blockIdx.x * WF_TRACE_BLOCK + o;
-            if (t.hitTri >= 0)
-                atomicMin(key, kind == 2 ? ((unsigned long long)__float_as_uint(t.tMax) << 32) |
-                                               ((unsigned long long)(hlp ? (link >> 8) : 0xFFu) << 24) | (uint32_t)t.hitTri
-                                         : 0ull);
-            __threadfence();
-            if ((atomicSub(&th_meta[o], 1u) & 0xFFFFu) == 1u && !WF_DIAG_NOSTORE) {
-                const unsigned long long k = atomicOr(key, 0ull);   // every part's update is in
-                if (kind == 2) b.hit[p] = k == ~0ull ? -1 : (int)(k & 0xFFFFFFull);
-                else b.occ[2 * (size_t)p + kind] = k != ~0ull ? 1 : 0;
-            }
-            busy = 0;
-        }
         // ---- refill: idle lanes take the wave's next queued rays; more passes when a
         // segment runs out part-way (wave-uniform control flow only)
         const int busy0 = WF_STATS ? __popcll(__ballot(busy != 0)) : 0;
@@ -1096,59 +1027,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
         };
         for (int pass = 0; pass < 4 && !exhausted && __ballot(busy == 0) != 0; ++pass) refill();
-        if (WF_TAIL_HELP && exhausted && s.n_tris < (1 << 24)) {
-            // ---- tail help: pair the i-th idle lane with the i-th owner that has a stealable entry
-            const uint64_t idleM = __ballot(busy == 0);
-            const uint32_t sp = t.spa >> WF_SPA_SHIFT;
-            const uint32_t meta = th_meta[threadIdx.x];
-            const uint32_t nx = (meta >> 16) & 0xFFu;
-            const bool cand = (busy != 0) && !(rid & WF_RID_HELPER) && nx < min(sp, (uint32_t)STK);
-            const uint64_t candM = __ballot(cand);
-            if (idleM != 0 && candM != 0) {
-                const uint32_t nI = (uint32_t)__popcll(idleM), nC = (uint32_t)__popcll(candM);
-                const uint32_t wbase = threadIdx.x & ~63u;
-                const bool helper = (busy == 0) && lanes_below(idleM) < nC;
-                const bool paired = cand && lanes_below(candM) < nI;
-                const int o = helper ? (int)kth_bit(candM, lanes_below(idleM)) : lane;
-                // the owner's ray and steal depth (every lane takes part in the shuffles)
-                const uint32_t od = (uint32_t)__shfl((int)nx, o);
-                const uint32_t orid = (uint32_t)__shfl((int)rid, o);
-                const float otmax = __shfl(t.tMax, o);
-                const int oany = __shfl((int)t.any, o);
-                RayP orr;
-                orr.o = mk3(__shfl(t.r.o.x, o), __shfl(t.r.o.y, o), __shfl(t.r.o.z, o));
-                orr.d = mk3(__shfl(t.r.d.x, o), __shfl(t.r.d.y, o), __shfl(t.r.d.z, o));
-                orr.inv = mk3(__shfl(t.r.inv.x, o), __shfl(t.r.inv.y, o), __shfl(t.r.inv.z, o));
-                orr.perm = __shfl(t.r.perm, o);
-                uint2 e = make_uint2(WF_STOLEN, 0u);
-                if (helper) e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + od * WF_SPA_STRIDE +
-                                                                8u * (wbase + (uint32_t)o));
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the helpers' reads before the owners' writes
-                if (paired) {           // give away the bottom-most stealable entry
-                    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + nx * WF_SPA_STRIDE + 8u * threadIdx.x) =
-                        make_uint2(WF_STOLEN, 0u);
-                    const uint32_t parts = (rid & WF_RID_SHARED) ? (meta & 0xFFFFu) + 1u : 2u;   // + owner itself
-                    th_meta[threadIdx.x] = ((nx + 1u) << 16) | parts;
-                    rid |= WF_RID_SHARED;
-                }
-                if (helper) {           // trace the stolen subtree with a copy of the owner's ray
-                    t.r = orr; t.tMax = otmax; t.any = oany != 0; t.hitTri = -1;
-                    t.spa = (uint32_t)threadIdx.x * 8u;
-                    const float z = __uint_as_float(e.y);
-                    const bool culled = t.r.cull_ok() & (z > t.tMax * 1.000001f) & (z > 1e-20f);
-                    const bool eLeaf = (e.x & REF_LEAF) != 0u;
-                    int es, ec;
-                    decode_leaf_fast(s, e.x, es, ec);
-                    t.lt = (!culled & eLeaf) ? es : 0;
-                    t.lc = (!culled & eLeaf) ? ec : 0;
-                    t.cur = (!culled & !eLeaf) ? e.x : REF_NONE;
-                    t.nst = 0;
-                    rid = (orid & ~WF_RID_HELPER) | WF_RID_SHARED | WF_RID_HELPER;
-                    th_link[threadIdx.x] = (uint16_t)((wbase + (uint32_t)o) | (od << 8));
-                    busy = 1;
-                }
-            }
-        }
         if (WF_STATS) { st[5] += 1; st[6] += __popcll(__ballot(busy != 0)) - busy0; }
         const uint64_t busym = __ballot(busy != 0);
         if (busym == 0) {
@@ -1161,7 +1039,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         auto run = [&](auto ident_tag) {
             for (;;) {
                 step_lane(ident_tag);
-                if (__popcll(__ballot(WF_TAIL_HELP ? busy == 1 : busy != 0)) <= thr) break;
+                if (__popcll(__ballot(busy != 0)) <= thr) break;
             }
         };
         if (__ballot(busy != 0 && t.r.kz() != 2) == 0) run(std::true_type{});
