@@ -671,7 +671,9 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool isNode = !isTri & (t.cur != REF_NONE);
     // ---- the step's single fetch: a triangle record or a node (lanes
     // with neither re-read node 0, which stays in L1)
-    const uint32_t off = isTri ? s.geo_tri_off + (uint32_t)t.lt * 48u : (isNode ? t.cur : 0u) * 64u;
+    // (an arithmetic select: written as ?: the compiler branches around the two halves)
+    const uint32_t offT = s.geo_tri_off + __umul24((uint32_t)t.lt, 48u), offN = (isNode ? t.cur : 0u) * 64u;
+    const uint32_t off = offN ^ ((offT ^ offN) & (0u - (uint32_t)isTri));
     // triangle lanes read the unused fourth quarter from one shared address
     // (one cache access per wave instead of one per lane)
     const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
