@@ -580,29 +580,38 @@ PN_DEV uint32_t wf_ovf_off(const WfBufs& b, uint32_t spa, int stk) {
     const uint32_t tl = (spa & (WF_SPA_STRIDE - 1u)) >> 3, k = (spa >> WF_SPA_SHIFT) - (uint32_t)stk;
     return ((blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride + k) * 8u;
 }
+// Push and pop run without branches around the LDS access: every lane of the
+// wave writes (push) or reads (pop) one LDS slot whether or not it moves its top
+// -- the free slot above the top, or, when that depth is in the spill area (or
+// the stack is empty), the lane's slot of one spare depth STK -- and only lanes
+// that push/pop move spa.  Only the rare spill-area access stays in a branch.
+// (Against a branch around the access: C2 +2.2 %, profiles/r03/ab_stack_bl_s11.txt.)
 template <int STK>
-PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, uint32_t ref, float z) {
+PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, bool push, uint32_t ref, float z) {
     const uint2 e = make_uint2(ref, __float_as_uint(z));
-    if (spa < STK * WF_SPA_STRIDE) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + spa) = e;
-    else b.ovf[wf_ovf_off(b, spa, STK) / 8u] = e;
-    spa += WF_SPA_STRIDE;
+    const bool inLds = spa < STK * WF_SPA_STRIDE;
+    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) +
+                              (inLds ? spa : STK * WF_SPA_STRIDE + (spa & (WF_SPA_STRIDE - 1u)))) = e;
+    if (push & !inLds) b.ovf[wf_ovf_off(b, spa, STK) / 8u] = e;
+    spa += push ? WF_SPA_STRIDE : 0u;
 }
 template <int STK>
-PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa) {
-    spa -= WF_SPA_STRIDE;
-    // the common case is a ds_read; the rare spill read is a buffer load, which the
-    // compiler cannot merge with the LDS read into one flat load (a flat load waits
-    // for every outstanding vector-memory operation, stores included)
-    uint2 e;
-    if (spa >= STK * WF_SPA_STRIDE) {
+PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa, bool pop) {
+    const uint32_t pa = spa - WF_SPA_STRIDE;      // wraps for an empty stack -> the spare slot
+    const bool inLds = pa < STK * WF_SPA_STRIDE;
+    uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) +
+                                              (inLds ? pa : STK * WF_SPA_STRIDE + (spa & (WF_SPA_STRIDE - 1u))));
+    // the spill read is a buffer load, which the compiler cannot merge with the
+    // LDS read into one flat load (a flat load waits for every outstanding
+    // vector-memory operation, stores included)
+    if (pop & !inLds) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)b.ovf, (short)0, 0x7fffffff, 0x00020000);
-        const uint32_t off = wf_ovf_off(b, spa, STK);
+        const uint32_t off = wf_ovf_off(b, pa, STK);
         e.x = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
         e.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off + 4, 0, 0);
-    } else {
-        e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + spa);
     }
+    spa = pop ? pa : spa;
     return e;
 }
 
@@ -665,8 +674,8 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // One step, written branch-light: the triangle test and the node
     // visit are both evaluated (a wave almost always holds lanes of
     // both kinds, so both paths ran anyway) and their results are
-    // selected per lane; only memory side effects (stack push/pop,
-    // the result store) and the rare IEEE division stay in branches.
+    // selected per lane; only the rare memory side effects (the stack's
+    // spill area, the result store) and the IEEE division stay in branches.
     const bool isTri = t.lc > 0;
     const bool isNode = !isTri & (t.cur != REF_NONE);
     // ---- the step's single fetch: a triangle record or a node (lanes
@@ -701,7 +710,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
     const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
     const float zFar = rightFirst ? zloL : zloR;
-    if (hNear & hFar) wf_push<STK>(lds, b, t.spa, farRef, zFar);
+    wf_push<STK>(lds, b, t.spa, hNear & hFar, farRef, zFar);
     const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
     int gs, gc;
@@ -712,16 +721,17 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // ---- next fetch target: pop when nothing is pending
     const bool idle = !done & (t.lc <= 0) & (t.cur == REF_NONE);
     done = done | (idle & (t.spa < WF_SPA_STRIDE));
-    if (idle & (t.spa >= WF_SPA_STRIDE)) {
-        const uint2 e = wf_pop<STK>(lds, b, t.spa);
+    {
+        const bool pop = idle & (t.spa >= WF_SPA_STRIDE);
+        const uint2 e = wf_pop<STK>(lds, b, t.spa, pop);
         const float z = __uint_as_float(e.y);
-        const bool culled = cull & (z > t.tMax * 1.000001f) & (z > 1e-20f);
+        const bool take = pop & !(cull & (z > t.tMax * 1.000001f) & (z > 1e-20f));
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
         int es, ec;
-        decode_leaf_fast(s, e.x, es, ec);
-        t.lt = (!culled & eLeaf) ? es : t.lt;
-        t.lc = (!culled & eLeaf) ? ec : t.lc;
-        t.cur = (!culled & !eLeaf) ? e.x : t.cur;
+        decode_leaf_fast(s, pop ? e.x : REF_NONE, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
+        t.lt = (take & eLeaf) ? es : t.lt;
+        t.lc = (take & eLeaf) ? ec : t.lc;
+        t.cur = (take & !eLeaf) ? e.x : t.cur;
     }
     return done;
 }
@@ -763,7 +773,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #endif
 template <int STK, bool SYNC>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
-    __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
+    __shared__ uint2 lds[(STK + 1) * WF_TRACE_BLOCK];     // STK depths + the spare one (wf_push)
     // nodes and triangle records through one buffer resource (32-bit offsets)
     const __amdgpu_buffer_rsrc_t geo =
         __builtin_amdgcn_make_buffer_rsrc((void*)s.nodes, (short)0, (int)s.geo_bytes, 0x00020000);
@@ -1098,7 +1108,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
 template <int STK>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_wf(DevScene s, FrameParams fp, WfBufs b,
                                                                                float4* rec) {
-    __shared__ uint2 lds[STK * WF_TRACE_BLOCK];
+    __shared__ uint2 lds[(STK + 1) * WF_TRACE_BLOCK];     // STK depths + the spare one (wf_push)
     const __amdgpu_buffer_rsrc_t geo =
         __builtin_amdgcn_make_buffer_rsrc((void*)s.nodes, (short)0, (int)s.geo_bytes, 0x00020000);
     const size_t npix = (size_t)fp.rows * fp.width;
