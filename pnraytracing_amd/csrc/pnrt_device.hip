@@ -343,8 +343,10 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
-            hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(trace_grid_for(c, b.n, alone)), dim3(WF_TRACE_BLOCK), 0,
-                               st, s, b, fp.mode);
+            const dim3 g(trace_grid_for(c, b.n, alone));
+            if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)
+                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false, true>), g, dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
+            else hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false, false>), g, dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
         }
         HIPCHK(c, hipGetLastError());
         if (WF_TIMING) {   // tail census: when the queue ran dry vs when the last wave ended
@@ -460,7 +462,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     pnrt_ctx::Pipe& P = c->pipe[pi];
     if (c->trace_grid == 0) {
         int per_cu = 0, cus = 0;
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false>, WF_TRACE_BLOCK, 0));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false, false>, WF_TRACE_BLOCK, 0));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
@@ -495,7 +497,9 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
             pb.ovf = P.ovf[0];
             pb.ovf_stride = (uint32_t)ovf_stride;
             const unsigned gp = (unsigned)std::min<size_t>((pix + WF_TRACE_BLOCK - 1) / WF_TRACE_BLOCK, (size_t)c->trace_grid);
-            hipLaunchKernelGGL((pt_primary_wf<WF_STACK>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w0, s, fp, pb, P.primary);
+            if (s.has_leaf_table)
+                hipLaunchKernelGGL((pt_primary_wf<WF_STACK, true>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w0, s, fp, pb, P.primary);
+            else hipLaunchKernelGGL((pt_primary_wf<WF_STACK, false>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w0, s, fp, pb, P.primary);
         } else {
             hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
         }
