@@ -787,7 +787,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         nodes[4 * k + 0] = make_float4(L[0], L[1], L[2], L[3]);
         nodes[4 * k + 1] = make_float4(L[4], L[5], R[0], R[1]);
         nodes[4 * k + 2] = make_float4(R[2], R[3], R[4], R[5]);
-        uint32_t meta[4] = {childref(i + 1), childref(rc), (uint32_t)fint(n[6]), 0u};
+        uint32_t meta[4] = {childref(i + 1), childref(rc), 16u << fint(n[6]), (uint32_t)fint(n[6])};
         std::memcpy(&nodes[4 * k + 3], meta, 16);
     }
     uint32_t root_ref = childref(0);

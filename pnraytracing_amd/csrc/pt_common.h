@@ -26,7 +26,7 @@
 //   n0 = (L.min.x, L.min.y, L.min.z, L.max.x)
 //   n1 = (L.max.y, L.max.z, R.min.x, R.min.y)
 //   n2 = (R.min.z, R.max.x, R.max.y, R.max.z)
-//   n3 = (refL, refR, axis, 0)                      (uints)
+//   n3 = (refL, refR, 16 << axis, axis)            (uints; the one-hot axis meets RayP::perm's sign bits)
 // child ref (32 bits): interior = node index; leaf = REF_LEAF | [29:7] first
 // triangle | [6:0] count, or REF_LEAF | REF_TABLE | index into leaf_table
 // (int2 start, count) when the range does not fit; REF_LEAF alone = empty.

@@ -21,7 +21,9 @@ struct RayP {
     f3 o, d;
     f3 inv;           // 1/dir (BoundIntersect :214); inv[kz] is the triangle test's invDz
     int perm;         // bits 0-1: kz of the axis permutation (:269-282; 2 = identity),
-                      // bit 2: z-slab culling is provably result-neutral for this ray
+                      // bit 2: z-slab culling is provably result-neutral for this ray,
+                      // bits 4-6: d.x < 0, d.y < 0, d.z < 0 (the near-child rule :448
+                      // against a node's one-hot axis 16 << axis: one AND)
     PN_DEV int kz() const { return perm & 3; }
     PN_DEV int kx() const { return (perm & 3) == 0 ? 2 : 0; }   // kz = 0: x <-> z swapped
     PN_DEV int ky() const { return (perm & 3) == 1 ? 2 : 1; }   // kz = 1: y <-> z swapped
@@ -40,7 +42,7 @@ PN_DEV RayP make_ray(f3 o, f3 d, int mode) {
     bool fin = pnm_fabs(o.x) < 1e6f && pnm_fabs(o.y) < 1e6f && pnm_fabs(o.z) < 1e6f &&
                pnm_fabs(d.x) < 1e6f && pnm_fabs(d.y) < 1e6f && pnm_fabs(d.z) < 1e6f;
     bool cull = (mode != 0) && fin && pnm_fabs(dz) >= 1e-12f;
-    r.perm = kz | (cull ? 4 : 0);
+    r.perm = kz | (cull ? 4 : 0) | (d.x < 0.0f ? 16 : 0) | (d.y < 0.0f ? 32 : 0) | (d.z < 0.0f ? 64 : 0);
     return r;
 }
 
@@ -137,7 +139,7 @@ PN_DEV bool traverse(const DevScene& s, const RayP& r, float& tMax, int& hitTri)
             bool hR = box_test(r, b.z, b.w, c.x, c.y, c.z, c.w, zloR, zhiR);
             if (hL && zcull(r, zloL, zhiL, tmc)) hL = false;
             if (hR && zcull(r, zloR, zhiR, tmc)) hR = false;
-            bool rightFirst = comp(r.d, (int)m.z) < 0;       // :448
+            bool rightFirst = comp(r.d, (int)m.w) < 0;       // :448
             uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
             bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
             float zFar = rightFirst ? zloL : zloR;

@@ -41,7 +41,7 @@ PN_DEV bool traverse_closest_lds(const DevScene& s, const RayP& r, float& tMax, 
             bool hR = box_test(r, b.z, b.w, c.x, c.y, c.z, c.w, zloR, zhiR);
             if (hL && zcull(r, zloL, zhiL, tmc)) hL = false;
             if (hR && zcull(r, zloR, zhiR, tmc)) hR = false;
-            bool rightFirst = comp(r.d, (int)m.z) < 0;       // :448
+            bool rightFirst = comp(r.d, (int)m.w) < 0;       // :448
             uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
             bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
             float zFar = rightFirst ? zloL : zloR;

@@ -666,7 +666,7 @@ struct TravState {
     float tMax;
     int hitTri, lt, lc;       // accepted triangle; pending triangle range [lt, lt + lc)
     uint32_t spa, cur;        // stack position (see wf_push); node to visit next
-    bool any;                 // any-hit (shadow) ray
+    uint32_t rid;             // kind << 30 | path: kinds 0 / 1 (shadow rays) are any-hit, kind 2 closest-hit
     uint32_t nst;             // WF_STATS builds: lane steps of this ray
 };
 
@@ -682,10 +682,11 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // spill area, the result store) and the IEEE division stay in branches.
     const bool isTri = t.lc > 0;
     const bool isNode = !isTri & (t.cur != REF_NONE);
-    // ---- the step's single fetch: a triangle record or a node (lanes
-    // with neither re-read node 0, which stays in L1)
+    // ---- the step's single fetch: a triangle record or a node; a lane with
+    // neither asks for REF_NONE * 64, beyond the buffer's range, so its loads
+    // return zeros without a cache access (it used to re-read node 0: +0.6 %)
     // (an arithmetic select: written as ?: the compiler branches around the two halves)
-    const uint32_t offT = s.geo_tri_off + __umul24((uint32_t)t.lt, 48u), offN = (isNode ? t.cur : 0u) * 64u;
+    const uint32_t offT = s.geo_tri_off + __umul24((uint32_t)t.lt, 48u), offN = t.cur * 64u;
     const uint32_t off = offN ^ ((offT ^ offN) & (0u - (uint32_t)isTri));
     // triangle lanes read the unused fourth quarter from one shared address
     // (one cache access per wave instead of one per lane)
@@ -696,8 +697,9 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     float e0, e1, e2, det, ts;
     const bool acc = tri_test<ID>(t.r, q0, q1, q2, t.tMax, e0, e1, e2, det, ts) & isTri;
     t.hitTri = acc ? t.lt : t.hitTri;
-    bool done = acc & t.any;
-    if (acc & !t.any) t.tMax = ts * (1.0f / det);
+    const bool any = t.rid < (2u << 30);      // (a compare, not a bool kept in a register)
+    bool done = acc & any;
+    if (acc & !any) t.tMax = ts * (1.0f / det);
     t.lt += isTri ? 1 : 0;
     t.lc -= isTri ? 1 : 0;
     // node visit: both child boxes (:447-457), z-slab culling
@@ -710,12 +712,15 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool cull = t.r.cull_ok();
     hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
     hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
-    const bool rightFirst = comp(t.r.d, (int)(m.z & 3u)) < 0;     // :448
+    const bool rightFirst = ((uint32_t)t.r.perm & m.z) != 0u;     // dir[axis] < 0 (:448; RayP::perm)
     const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
-    const bool hNear = rightFirst ? hR : hL, hFar = rightFirst ? hL : hR;
     const float zFar = rightFirst ? zloL : zloR;
-    wf_push<STK>(lds, b, t.spa, hNear & hFar, farRef, zFar);
-    const uint32_t go = hNear ? nearRef : (hFar ? farRef : REF_NONE);
+    // both children hit: continue with the near one, push the far one; one hit:
+    // continue with it (the same choice as selecting near / far flags by
+    // rightFirst, without turning those flags into selected values)
+    const bool both = hL & hR;
+    wf_push<STK>(lds, b, t.spa, both, farRef, zFar);
+    const uint32_t go = both ? nearRef : (hL ? m.x : (hR ? m.y : REF_NONE));
     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
     int gs, gc;
     decode_leaf_fast<TBL>(s, go, gs, gc);
@@ -732,7 +737,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
         const bool take = pop & !(cull & (z > t.tMax * 1.000001f) & (z > 1e-20f));
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
         int es, ec;
-        decode_leaf_fast<TBL>(s, pop ? e.x : REF_NONE, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
+        decode_leaf_fast<TBL>(s, (TBL && !pop) ? REF_NONE : e.x, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
         t.lt = (take & eLeaf) ? es : t.lt;
         t.lc = (take & eLeaf) ? ec : t.lc;
         t.cur = (take & !eLeaf) ? e.x : t.cur;
@@ -801,8 +806,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     t.hitTri = -1; t.lt = 0; t.lc = 0;
     t.spa = (uint32_t)threadIdx.x * 8u;      // stack position (see wf_push)
     t.cur = REF_NONE;
-    t.any = true;
-    uint32_t rid = 0;
+    t.rid = 0u;
     int busy = 0;
     // Ray accounting: when the block's last wave leaves, every ray the block took
     // off the global queue must have been loaded into a lane (a loaded ray is always
@@ -970,7 +974,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             st[1] += __popcll(__ballot(busy != 0));
             st[2] += __popcll(__ballot(busy != 0 && t.lc > 0));
             st[3] += __popcll(__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE));
-            st[7] += __popcll(__ballot(busy != 0 && (rid >> 30) == 2u));     // continuation-ray lane steps
+            st[7] += __popcll(__ballot(busy != 0 && (t.rid >> 30) == 2u));     // continuation-ray lane steps
             {   // steps whose fetch address is the same for every active lane
                 const uint64_t act = __ballot(busy != 0);
                 const uint32_t fo = t.lc > 0 ? 0x80000000u + (uint32_t)t.lt : t.cur;
@@ -982,10 +986,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         if (busy) {
             const bool done = wf_step<STK, ID, TBL>(s, b, geo, lds, t);
             if (WF_STATS || WF_TIMING) t.nst += 1;
-            if (WF_STATS && done) atomicAdd(&hist[(rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
-            if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (rid >> 30) << 16 | min(t.nst, 0xffffu);
+            if (WF_STATS && done) atomicAdd(&hist[(t.rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
+            if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (t.rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
-                const uint32_t kind = rid >> 30, p = rid & 0x3fffffffu;
+                const uint32_t kind = t.rid >> 30, p = t.rid & 0x3fffffffu;
                 if (!WF_DIAG_NOSTORE) {
                     if (kind == 2) b.hit[p] = t.hitTri;
                     else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
@@ -1035,7 +1039,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                         root = s.root_ref;
                         if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
                     }
-                    t.r = nr; t.tMax = ntmax; t.any = nany; rid = (kind << 30) | p;
+                    t.r = nr; t.tMax = ntmax; t.rid = (kind << 30) | p;
                     t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
                     t.nst = 0;
                     busy = 1;
@@ -1129,7 +1133,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_w
         t.hitTri = -1; t.lt = 0; t.lc = 0;
         t.spa = (uint32_t)threadIdx.x * 8u;
         t.cur = REF_NONE;
-        t.any = false;
+        t.rid = 2u << 30;       // closest hit
         float zlo;
         if (mine && box_fast(t.r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
                              s.root_max[2], zlo)) {
