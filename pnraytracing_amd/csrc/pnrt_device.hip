@@ -87,6 +87,7 @@ struct pnrt_ctx {
     bool has_frame = false;
     float4* accum = nullptr;
     int mode = PNRT_TRAVERSE_ZCULL;
+    bool boxes_finite = true;              // every BVH box coordinate finite: z-slab culling allowed (pt_wf.h box_slabs)
     int kernel = 3;                        // 3 = wavefront (default), 1 = v1 one-lane-per-pixel
     bool serial = false;                   // PNRT_SERIAL: one call in flight, full trace grid (measurement)
     // Pipelined wavefront rendering.  pnrt_render calls rotate over the pipes -- the
@@ -834,7 +835,6 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         s.nodes = static_cast<const float4*>(g);
         s.tris = reinterpret_cast<const float4*>(static_cast<char*>(g) + nb);
         s.geo_tri_off = (uint32_t)nb;
-        s.geo_zero_off = (uint32_t)(nb + (size_t)nt * 48);      // tris' zeroed tail record
         s.geo_bytes = (uint32_t)(nb + tb);
     }
     if ((rc = upload(c, leaf_table, &s.leaf_table)) || (rc = upload(c, tidx, &s.tri_idx)) ||
@@ -846,6 +846,13 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     s.lights_sum_area = lsum;
     const float* root = N;
     for (int k = 0; k < 3; ++k) { s.root_min[k] = root[k]; s.root_max[k] = root[3 + k]; }
+    // z-slab culling's proof needs finite boxes (then a culling-enabled ray's
+    // z-slab distances are never NaN); a scene with a non-finite box coordinate
+    // is traversed without culling, which is the reference's exact traversal
+    c->boxes_finite = true;
+    for (size_t i = 0; i < (size_t)nn && c->boxes_finite; ++i)
+        for (int k = 0; k < 6; ++k)
+            if (!std::isfinite(N[12 * i + k])) { c->boxes_finite = false; break; }
     s.root_ref = root_ref;
     s.has_leaf_table = has_leaf_table;
     {   // GetLightIndex is a lower bound: a linear scan returns the same index iff the
@@ -1034,7 +1041,7 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
     fp.first_frame = first; fp.n_frames = nf;
     fp.band = band; fp.n_shards = nsh; fp.shard = shard;
     fp.rows = shard_rows(c->height, band, nsh, shard);
-    fp.mode = c->mode;
+    fp.mode = c->boxes_finite ? c->mode : PNRT_TRAVERSE_EXACT;
     if (fp.rows == 0) return PNRT_OK;
     DevScene s = c->scene;
     s.hdr = static_cast<const float4*>(c->hdr);

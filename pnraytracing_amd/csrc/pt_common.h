@@ -48,8 +48,8 @@ struct DevScene {
     const float2* lights;       // (index as float, prefixArea) as uploaded, zero-padded to >= 8 entries
     const float4* tri_attr;     // 4 float4 / triangle (BVH order): n0 n1 n2 uv0 uv1 uv2 of its vertices
     uint32_t geo_tri_off;       // nodes and tris share one allocation (nodes first): byte offset of tris,
-    uint32_t geo_zero_off;      // of the zero float4 after the last triangle record,
-    uint32_t geo_bytes;         // and its size (< 4 GiB: 32-bit buffer offsets in the trace kernel)
+    uint32_t geo_bytes;         // and its size (< 4 GiB - 64: 32-bit buffer offsets in the trace kernel,
+                                // whose offsets >= 0xffffffc0 fall outside the range and read zeros)
     const float4* zero4;        // one float4 (0, 0, 0, 0): the load target of lanes that need no data
     const float4* light_rec;    // 7 float4 / light entry (+1 for triangle 0): its triangle's vertex
                                 // records va0 vb0 va1 vb1 va2 vb2 and (emission, 0)

@@ -138,7 +138,7 @@ struct WfBufs {
     // trace results, by path entry j
     uint8_t* occ;      // [2 * n]: light, env occluded
     int* hit;          // continuation hit triangle or -1
-    uint2* ovf;        // traversal stack spill, ovf_stride entries per trace lane
+    uint2* ovf;        // traversal stack spill: per trace block ovf_stride depths x 2048 B (wf_ovf_rsrc)
     uint32_t ovf_stride;
     unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
     // ray queues, written by setup without atomics: segment (k, j) of kind k
@@ -578,42 +578,48 @@ PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& c
 // byte address of entry sp of lane tl (entries of one depth are 2048 B apart,
 // 256 lanes x 8 B; WF_SPA_STRIDE in general), so sp = spa >> 11 and the lane's slot is spa & 2047 -- no
 // separate per-lane base register (at 8 waves/SIMD the compiler spilled it).
-// Entries deeper than STK go to the global spill area, addressed from the same
-// value through one block-uniform buffer resource.
-PN_DEV uint32_t wf_ovf_off(const WfBufs& b, uint32_t spa, int stk) {
-    const uint32_t tl = (spa & (WF_SPA_STRIDE - 1u)) >> 3, k = (spa >> WF_SPA_SHIFT) - (uint32_t)stk;
-    return ((blockIdx.x * WF_TRACE_BLOCK + tl) * b.ovf_stride + k) * 8u;
+// Entries deeper than STK go to the block's region of the global spill area
+// (ovf_stride depths x 2048 B), laid out like the LDS stack, so the buffer
+// access takes spa itself as its per-lane offset: the resource starts STK
+// depths before the area and the block's region is the access's scalar
+// offset -- no per-lane address arithmetic (the lane-major layout cost 2 VALU
+// per step, hoisted out of the rare spill branches by the compiler).
+PN_DEV __amdgpu_buffer_rsrc_t wf_ovf_rsrc(const WfBufs& b, int stk) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((char*)b.ovf - (size_t)stk * WF_SPA_STRIDE), (short)0, 0x7fffffff,
+                                             0x00020000);
 }
+PN_DEV int wf_ovf_soff(const WfBufs& b) { return (int)(blockIdx.x * b.ovf_stride * WF_SPA_STRIDE); }
 // Push and pop run without branches around the LDS access: every lane of the
 // wave writes (push) or reads (pop) one LDS slot whether or not it moves its top
 // -- the free slot above the top, or, when that depth is in the spill area (or
-// the stack is empty), the lane's slot of one spare depth STK -- and only lanes
-// that push/pop move spa.  Only the rare spill-area access stays in a branch.
+// the stack is empty), the lane's slot of one spare depth STK (the minimum of
+// the two addresses) -- and only lanes that push/pop move spa.  Only the rare
+// spill-area access stays in a branch.
 // (Against a branch around the access: C2 +2.2 %, profiles/r03/ab_stack_bl_s11.txt.)
 template <int STK>
+PN_DEV uint32_t wf_spare(uint32_t spa) { return (STK * WF_SPA_STRIDE) | (spa & (WF_SPA_STRIDE - 1u)); }
+template <int STK>
 PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, bool push, uint32_t ref, float z) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     const uint2 e = make_uint2(ref, __float_as_uint(z));
-    const bool inLds = spa < STK * WF_SPA_STRIDE;
-    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) +
-                              (inLds ? spa : STK * WF_SPA_STRIDE + (spa & (WF_SPA_STRIDE - 1u)))) = e;
-    if (push & !inLds) b.ovf[wf_ovf_off(b, spa, STK) / 8u] = e;
+    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + min(spa, wf_spare<STK>(spa))) = e;
+    if (push & (spa >= STK * WF_SPA_STRIDE)) {
+        const u2 v = {e.x, e.y};
+        __builtin_amdgcn_raw_buffer_store_b64(v, wf_ovf_rsrc(b, STK), (int)spa, wf_ovf_soff(b), 0);
+    }
     spa += push ? WF_SPA_STRIDE : 0u;
 }
 template <int STK>
 PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa, bool pop) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     const uint32_t pa = spa - WF_SPA_STRIDE;      // wraps for an empty stack -> the spare slot
-    const bool inLds = pa < STK * WF_SPA_STRIDE;
-    uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) +
-                                              (inLds ? pa : STK * WF_SPA_STRIDE + (spa & (WF_SPA_STRIDE - 1u))));
+    uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + min(pa, wf_spare<STK>(spa)));
     // the spill read is a buffer load, which the compiler cannot merge with the
     // LDS read into one flat load (a flat load waits for every outstanding
     // vector-memory operation, stores included)
-    if (pop & !inLds) {
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)b.ovf, (short)0, 0x7fffffff, 0x00020000);
-        const uint32_t off = wf_ovf_off(b, pa, STK);
-        e.x = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
-        e.y = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off + 4, 0, 0);
+    if (pop & (pa >= STK * WF_SPA_STRIDE)) {
+        const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)pa, wf_ovf_soff(b), 0);
+        e = make_uint2(v.x, v.y);
     }
     spa = pop ? pa : spa;
     return e;
@@ -631,7 +637,11 @@ PN_DEV bool box_slabs(const RayP& r, float fx, float fy, float fz, float nx, flo
     const int kz = IDENT ? 2 : r.kz();
     float zf = kz == 2 ? fz : (kz == 0 ? fx : fy);
     float zn = kz == 2 ? nz : (kz == 0 ? nx : ny);
-    float lo = zn < zf ? zn : zf, hi = zn < zf ? zf : zn;
+    // the z-slab ends only matter for culling-enabled rays, whose z-slab
+    // distances are never NaN (finite ray, |d_kz| >= 1e-12, finite boxes: the
+    // host disables culling otherwise), so min / max equal the compare-selects
+    // of pt_kernel.h box_test -- and for kz = 2 they are the t0 / t1 terms above
+    float lo = fminf(zn, zf), hi = fmaxf(zn, zf);
     zlo = lo;
     // zhi <= 0: the whole box is behind the ray in the triangle test's frame
     return (t1 >= t0) & !(r.cull_ok() & (hi <= 0.0f));
@@ -644,6 +654,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return box_slabs<IDENT>(r, fx, fy, fz, nx, ny, nz, zlo);
 }
 
+#ifndef WF_DIV_ALL
+#define WF_DIV_ALL 0
+#endif
 #ifndef WF_BLOCKQ
 #define WF_BLOCKQ 1         // block-level ray queue shared by a block's waves (see the trace kernel)
 #endif
@@ -688,9 +701,9 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // (an arithmetic select: written as ?: the compiler branches around the two halves)
     const uint32_t offT = s.geo_tri_off + __umul24((uint32_t)t.lt, 48u), offN = t.cur * 64u;
     const uint32_t off = offN ^ ((offT ^ offN) & (0u - (uint32_t)isTri));
-    // triangle lanes read the unused fourth quarter from one shared address
-    // (one cache access per wave instead of one per lane)
-    const uint32_t off3 = isTri ? s.geo_zero_off : off + 48u;
+    // triangle lanes need no fourth quarter: theirs lies beyond the buffer's
+    // range too (zeros, no cache access; it used to be one shared address)
+    const uint32_t off3 = isTri ? 0xfffffff0u : off + 48u;
     const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
                  q3 = geo_load(geo, off3);
     // triangle test (:254-357 / :360-424)
@@ -699,7 +712,16 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     t.hitTri = acc ? t.lt : t.hitTri;
     const bool any = t.rid < (2u << 30);      // (a compare, not a bool kept in a register)
     bool done = acc & any;
+#if WF_DIV_ALL
+    {   // every lane divides (IEEE; a lane that accepts nothing may divide by zero,
+        // harmlessly) and the accepted closest-hit lanes take the quotient
+        float q = ts * (1.0f / det);
+        asm volatile("" : "+v"(q));     // (or the compiler sinks the division into a branch)
+        t.tMax = (acc & !any) ? q : t.tMax;
+    }
+#else
     if (acc & !any) t.tMax = ts * (1.0f / det);
+#endif
     t.lt += isTri ? 1 : 0;
     t.lc -= isTri ? 1 : 0;
     // node visit: both child boxes (:447-457), z-slab culling
@@ -983,9 +1005,13 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
         }
         if (WF_TIMING) ++witer;
-        if (busy) {
-            const bool done = wf_step<STK, ID, TBL>(s, b, geo, lds, t);
-            if (WF_STATS || WF_TIMING) t.nst += 1;
+        // every lane steps: a lane without a ray holds a finished state (nothing
+        // pending, empty stack), whose step fetches beyond the buffer's range,
+        // tests nothing and touches only its own free LDS slot -- no branch
+        // around the step (against `if (busy)`: C2 +3.5 %, trace -4 %)
+        {
+            const bool done = wf_step<STK, ID, TBL>(s, b, geo, lds, t) & (busy != 0);
+            if (WF_STATS || WF_TIMING) t.nst += busy ? 1 : 0;
             if (WF_STATS && done) atomicAdd(&hist[(t.rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (t.rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
@@ -995,6 +1021,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
                 }
                 busy = 0;
+                t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;     // (an any-hit ray may stop mid-tree)
             }
         }
 #if WF_DIAG_VALU
@@ -1144,7 +1171,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_w
         auto run = [&](auto ident_tag) {
             constexpr bool ID = decltype(ident_tag)::value;
             for (;;) {
-                if (busy && wf_step<STK, ID, TBL>(s, b, geo, lds, t)) busy = 0;
+                if (wf_step<STK, ID, TBL>(s, b, geo, lds, t)) busy = 0;     // (a finished lane's step is a no-op)
                 if (__ballot(busy != 0) == 0) break;
             }
         };
