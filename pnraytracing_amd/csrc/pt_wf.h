@@ -597,12 +597,12 @@ PN_DEV int wf_ovf_soff(const WfBufs& b) { return (int)(blockIdx.x * b.ovf_stride
 // spill-area access stays in a branch.
 // (Against a branch around the access: C2 +2.2 %, profiles/r03/ab_stack_bl_s11.txt.)
 template <int STK>
-PN_DEV uint32_t wf_spare(uint32_t spa) { return (STK * WF_SPA_STRIDE) | (spa & (WF_SPA_STRIDE - 1u)); }
+PN_DEV uint32_t wf_spare() { return (STK * WF_SPA_STRIDE) | (threadIdx.x * 8u); }   // (= its spa & 2047, kept live: 2 VALU per step less)
 template <int STK>
 PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, bool push, uint32_t ref, float z) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     const uint2 e = make_uint2(ref, __float_as_uint(z));
-    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + min(spa, wf_spare<STK>(spa))) = e;
+    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + min(spa, wf_spare<STK>())) = e;
     if (push & (spa >= STK * WF_SPA_STRIDE)) {
         const u2 v = {e.x, e.y};
         __builtin_amdgcn_raw_buffer_store_b64(v, wf_ovf_rsrc(b, STK), (int)spa, wf_ovf_soff(b), 0);
@@ -613,7 +613,7 @@ template <int STK>
 PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa, bool pop) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     const uint32_t pa = spa - WF_SPA_STRIDE;      // wraps for an empty stack -> the spare slot
-    uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + min(pa, wf_spare<STK>(spa)));
+    uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + min(pa, wf_spare<STK>()));
     // the spill read is a buffer load, which the compiler cannot merge with the
     // LDS read into one flat load (a flat load waits for every outstanding
     // vector-memory operation, stores included)
@@ -654,9 +654,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return box_slabs<IDENT>(r, fx, fy, fz, nx, ny, nz, zlo);
 }
 
-#ifndef WF_DIV_ALL
-#define WF_DIV_ALL 0
-#endif
 #ifndef WF_BLOCKQ
 #define WF_BLOCKQ 1         // block-level ray queue shared by a block's waves (see the trace kernel)
 #endif
@@ -712,37 +709,31 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     t.hitTri = acc ? t.lt : t.hitTri;
     const bool any = t.rid < (2u << 30);      // (a compare, not a bool kept in a register)
     bool done = acc & any;
-#if WF_DIV_ALL
-    {   // every lane divides (IEEE; a lane that accepts nothing may divide by zero,
-        // harmlessly) and the accepted closest-hit lanes take the quotient
-        float q = ts * (1.0f / det);
-        asm volatile("" : "+v"(q));     // (or the compiler sinks the division into a branch)
-        t.tMax = (acc & !any) ? q : t.tMax;
-    }
-#else
     if (acc & !any) t.tMax = ts * (1.0f / det);
-#endif
     t.lt += isTri ? 1 : 0;
     t.lc -= isTri ? 1 : 0;
     // node visit: both child boxes (:447-457), z-slab culling
     const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
                                __float_as_uint(q3.w));
+    // z > tMax * (1 + 1e-6) and z > 1e-20 as one compare: against the larger of
+    // the two, keeping a NaN tMax (then nothing is culled, as before)
     const float tmc = t.tMax * 1.000001f;
+    const float zc = tmc <= 1e-20f ? 1e-20f : tmc;
     float zloL, zloR;
     bool hL = box_fast<ID>(t.r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
     bool hR = box_fast<ID>(t.r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
     const bool cull = t.r.cull_ok();
-    hL = hL & !(cull & (zloL > tmc) & (zloL > 1e-20f)) & isNode;
-    hR = hR & !(cull & (zloR > tmc) & (zloR > 1e-20f)) & isNode;
+    hL = hL & !(cull & (zloL > zc)) & isNode;
+    hR = hR & !(cull & (zloR > zc)) & isNode;
     const bool rightFirst = ((uint32_t)t.r.perm & m.z) != 0u;     // dir[axis] < 0 (:448; RayP::perm)
-    const uint32_t nearRef = rightFirst ? m.y : m.x, farRef = rightFirst ? m.x : m.y;
+    const uint32_t farRef = rightFirst ? m.x : m.y;
     const float zFar = rightFirst ? zloL : zloR;
     // both children hit: continue with the near one, push the far one; one hit:
-    // continue with it (the same choice as selecting near / far flags by
-    // rightFirst, without turning those flags into selected values)
+    // continue with it.  The right child is taken when it is hit and either the
+    // left one is not or the right one is the near one -- one mask, two selects
     const bool both = hL & hR;
     wf_push<STK>(lds, b, t.spa, both, farRef, zFar);
-    const uint32_t go = both ? nearRef : (hL ? m.x : (hR ? m.y : REF_NONE));
+    const uint32_t go = (hR & (!hL | rightFirst)) ? m.y : (hL ? m.x : REF_NONE);
     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
     int gs, gc;
     decode_leaf_fast<TBL>(s, go, gs, gc);
@@ -756,7 +747,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
         const bool pop = idle & (t.spa >= WF_SPA_STRIDE);
         const uint2 e = wf_pop<STK>(lds, b, t.spa, pop);
         const float z = __uint_as_float(e.y);
-        const bool take = pop & !(cull & (z > t.tMax * 1.000001f) & (z > 1e-20f));
+        const bool take = pop & !(cull & (z > zc));     // (zc: tMax after this step's acceptance, as before)
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
         int es, ec;
         decode_leaf_fast<TBL>(s, (TBL && !pop) ? REF_NONE : e.x, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
