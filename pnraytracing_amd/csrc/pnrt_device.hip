@@ -765,13 +765,20 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         if (fint(N[12 * (size_t)(i + 1) + 7]) != -1) order.push_back(i + 1);
         if (fint(N[12 * (size_t)rc + 7]) != -1) order.push_back(rc);
     }
-    // packed child reference (pt_common.h): interior -> node index, leaf -> range
+    // child reference (pt_common.h): interior -> node index, leaf -> range, in the
+    // packed encoding when every leaf fits it, else the wide one (+ leaf table)
+    bool packed = nt < (1 << 24) - 1;
+    for (size_t i = 0; i < (size_t)nn && packed; ++i) {
+        const float* n = N + 12 * i;
+        if (fint(n[7]) == -1 && fint(n[9]) - fint(n[8]) > 127) packed = false;
+    }
     std::vector<int2> leaf_table;
     auto childref = [&](int ci) -> uint32_t {
         const float* n = N + 12 * (size_t)ci;
         if (fint(n[7]) != -1) return (uint32_t)dn[ci];
         int s0 = fint(n[8]), cnt = fint(n[9]) - s0;
         if (cnt <= 0) return REF_LEAF;
+        if (packed) return REF_LEAF | ((uint32_t)cnt << 24) | (uint32_t)s0;
         if (cnt <= 127 && s0 < (1 << 23)) return REF_LEAF | ((uint32_t)s0 << 7) | (uint32_t)cnt;
         leaf_table.push_back(make_int2(s0, cnt));
         return REF_LEAF | REF_TABLE | (uint32_t)(leaf_table.size() - 1);
@@ -792,7 +799,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         std::memcpy(&nodes[4 * k + 3], meta, 16);
     }
     uint32_t root_ref = childref(0);
-    const int has_leaf_table = leaf_table.empty() ? 0 : 1;
+    const int has_leaf_table = packed ? 0 : 1;
     if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
     // trace-kernel stack bound: at most one deferred sibling per BVH level
     c->wf_stack_need = maxd + 2;

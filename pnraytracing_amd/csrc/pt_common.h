@@ -27,9 +27,14 @@
 //   n1 = (L.max.y, L.max.z, R.min.x, R.min.y)
 //   n2 = (R.min.z, R.max.x, R.max.y, R.max.z)
 //   n3 = (refL, refR, 16 << axis, axis)            (uints; the one-hot axis meets RayP::perm's sign bits)
-// child ref (32 bits): interior = node index; leaf = REF_LEAF | [29:7] first
-// triangle | [6:0] count, or REF_LEAF | REF_TABLE | index into leaf_table
-// (int2 start, count) when the range does not fit; REF_LEAF alone = empty.
+// child ref (32 bits): interior = node index; REF_LEAF alone = an empty leaf.
+// A leaf's triangle range [first, first + count) has one of two encodings, per
+// scene (DevScene::has_leaf_table):
+//   packed (every leaf's count <= 127, fewer than 2^24 - 1 triangles):
+//     REF_LEAF | count << 24 | first -- the trace step keeps this word as its
+//     pending range (pt_wf.h wf_has_tri);
+//   wide (otherwise): REF_LEAF | [29:7] first | [6:0] count, or REF_LEAF |
+//     REF_TABLE | index into leaf_table (int2 first, count) when that does not fit.
 // Boxes are the reference floats bit for bit.
 // Triangle (BVH order), 48 B: t0 = (p0.xyz, p1.x), t1 = (p1.yz, p2.xy),
 //   t2 = (p2.z, matId, texId, -) ; tri_idx = (i0, i1, i2, -)
@@ -57,7 +62,7 @@ struct DevScene {
     float lights_sum_area;
     float root_min[3], root_max[3];
     uint32_t root_ref;
-    int has_leaf_table;         // some leaf range needed the table (REF_TABLE refs exist)
+    int has_leaf_table;         // the wide leaf encoding (REF_TABLE refs may exist); 0: packed (pt_common.h)
     int light_scan;             // <= PT_LIGHT_SCAN lights with non-decreasing prefix areas
     float lscan[PT_LIGHT_SCAN]; // their prefix areas, passed by value: scalar (kernel-argument) loads
     int has_hdr, hdr_w, hdr_h;

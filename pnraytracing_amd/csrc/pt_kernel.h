@@ -104,7 +104,12 @@ PN_DEV bool tri_test(const RayP& r, const float4& t0, const float4& t1, const fl
 }
 
 PN_DEV void decode_leaf(const DevScene& s, uint32_t ref, int& start, int& cnt) {
-    if (ref & REF_TABLE) {
+    if (!s.has_leaf_table) {            // packed encoding (pt_common.h)
+        // (an opaque mask: see pt_wf.h wf_tri_index -- a plain one was dropped
+        // ahead of a 64-bit address multiply)
+        asm("v_and_b32 %0, 0xffffff, %1" : "=v"(start) : "v"(ref));
+        cnt = (int)((ref >> 24) & 0x7fu);
+    } else if (ref & REF_TABLE) {
         int2 e = s.leaf_table[ref & 0x3fffffffu];
         start = e.x; cnt = e.y;
     } else {

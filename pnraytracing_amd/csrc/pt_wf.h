@@ -671,6 +671,12 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 }
 
 // One lane's traversal state (a ray being traced).
+// The pending triangle range: in a wide-encoding scene (TBL) lt = first, lc =
+// count; in a packed one (pt_common.h) lt holds the range as its leaf ref,
+// REF_LEAF | count << 24 | first, and lc is unused -- the word a node or the
+// stack supplies is the state itself (no decode), a pending triangle is one
+// compare, a step one add, and the fetch offset's mad_u24 reads the first
+// triangle from the low 24 bits; hitTri is then such a word too (or -1).
 struct TravState {
     RayP r;
     float tMax;
@@ -679,6 +685,21 @@ struct TravState {
     uint32_t rid;             // kind << 30 | path: kinds 0 / 1 (shadow rays) are any-hit, kind 2 closest-hit
     uint32_t nst;             // WF_STATS builds: lane steps of this ray
 };
+
+template <bool TBL>
+PN_DEV bool wf_has_tri(const TravState& t) { return TBL ? t.lc > 0 : (uint32_t)t.lt >= (REF_LEAF | (1u << 24)); }
+// The triangle index of an accepted-hit word.  The mask goes through an opaque
+// v_and: with a plain `h & 0xffffff` feeding a 64-bit address (hit_fetch) this
+// compiler (ROCm 7.2 clang, gfx950) emitted v_mad_u64_u32 on the UNMASKED word
+// -- the mask dropped as if the multiply were a 24-bit one -- and the primary
+// pass read far outside the triangle array (a GPU memory fault).
+template <bool TBL>
+PN_DEV int wf_tri_index(int h) {
+    if (TBL || h == -1) return h;
+    int r;
+    asm("v_and_b32 %0, 0xffffff, %1" : "=v"(r) : "v"(h));
+    return r;
+}
 
 // One traversal step of a lane's ray; returns true when the ray is finished
 // (an any-hit ray accepted a triangle, or nothing is left to visit).
@@ -690,17 +711,18 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // both kinds, so both paths ran anyway) and their results are
     // selected per lane; only the rare memory side effects (the stack's
     // spill area, the result store) and the IEEE division stay in branches.
-    const bool isTri = t.lc > 0;
-    const bool isNode = !isTri & (t.cur != REF_NONE);
+    const bool isTri = wf_has_tri<TBL>(t);
+    const bool isNode = t.cur != REF_NONE;     // (a lane with pending triangles has cur = REF_NONE)
     // ---- the step's single fetch: a triangle record or a node; a lane with
     // neither asks for REF_NONE * 64, beyond the buffer's range, so its loads
     // return zeros without a cache access (it used to re-read node 0: +0.6 %)
     // (an arithmetic select: written as ?: the compiler branches around the two halves)
     const uint32_t offT = s.geo_tri_off + __umul24((uint32_t)t.lt, 48u), offN = t.cur * 64u;
     const uint32_t off = offN ^ ((offT ^ offN) & (0u - (uint32_t)isTri));
-    // triangle lanes need no fourth quarter: theirs lies beyond the buffer's
-    // range too (zeros, no cache access; it used to be one shared address)
-    const uint32_t off3 = isTri ? 0xfffffff0u : off + 48u;
+    // triangle lanes need no fourth quarter: their cur is REF_NONE (entering a
+    // leaf clears it), so offN + 48 lies beyond the buffer's range too (zeros, no
+    // cache access; it used to be one shared address)
+    const uint32_t off3 = offN + 48u;
     const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
                  q3 = geo_load(geo, off3);
     // triangle test (:254-357 / :360-424)
@@ -710,8 +732,12 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool any = t.rid < (2u << 30);      // (a compare, not a bool kept in a register)
     bool done = acc & any;
     if (acc & !any) t.tMax = ts * (1.0f / det);
-    t.lt += isTri ? 1 : 0;
-    t.lc -= isTri ? 1 : 0;
+    if (TBL) {
+        t.lt += isTri ? 1 : 0;
+        t.lc -= isTri ? 1 : 0;
+    } else {
+        t.lt += isTri ? (int)(1u - (1u << 24)) : 0;     // first + 1, count - 1
+    }
     // node visit: both child boxes (:447-457), z-slab culling
     const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
                                __float_as_uint(q3.w));
@@ -735,13 +761,17 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     wf_push<STK>(lds, b, t.spa, both, farRef, zFar);
     const uint32_t go = (hR & (!hL | rightFirst)) ? m.y : (hL ? m.x : REF_NONE);
     const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
-    int gs, gc;
-    decode_leaf_fast<TBL>(s, go, gs, gc);
-    t.lt = goLeaf ? gs : t.lt;
-    t.lc = goLeaf ? gc : t.lc;
+    if (TBL) {
+        int gs, gc;
+        decode_leaf_fast<TBL>(s, go, gs, gc);
+        t.lt = goLeaf ? gs : t.lt;
+        t.lc = goLeaf ? gc : t.lc;
+    } else {
+        t.lt = goLeaf ? (int)go : t.lt;
+    }
     t.cur = isNode ? (goLeaf ? REF_NONE : go) : t.cur;
     // ---- next fetch target: pop when nothing is pending
-    const bool idle = !done & (t.lc <= 0) & (t.cur == REF_NONE);
+    const bool idle = !done & !wf_has_tri<TBL>(t) & (t.cur == REF_NONE);
     done = done | (idle & (t.spa < WF_SPA_STRIDE));
     {
         const bool pop = idle & (t.spa >= WF_SPA_STRIDE);
@@ -749,10 +779,14 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
         const float z = __uint_as_float(e.y);
         const bool take = pop & !(cull & (z > zc));     // (zc: tMax after this step's acceptance, as before)
         const bool eLeaf = (e.x & REF_LEAF) != 0u;
-        int es, ec;
-        decode_leaf_fast<TBL>(s, (TBL && !pop) ? REF_NONE : e.x, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
-        t.lt = (take & eLeaf) ? es : t.lt;
-        t.lc = (take & eLeaf) ? ec : t.lc;
+        if (TBL) {
+            int es, ec;
+            decode_leaf_fast<TBL>(s, pop ? e.x : REF_NONE, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
+            t.lt = (take & eLeaf) ? es : t.lt;
+            t.lc = (take & eLeaf) ? ec : t.lc;
+        } else {
+            t.lt = (take & eLeaf) ? (int)e.x : t.lt;
+        }
         t.cur = (take & !eLeaf) ? e.x : t.cur;
     }
     return done;
@@ -985,12 +1019,12 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         if (WF_STATS) {
             st[0] += 1;
             st[1] += __popcll(__ballot(busy != 0));
-            st[2] += __popcll(__ballot(busy != 0 && t.lc > 0));
-            st[3] += __popcll(__ballot(busy != 0 && t.lc <= 0 && t.cur != REF_NONE));
+            st[2] += __popcll(__ballot(busy != 0 && wf_has_tri<TBL>(t)));
+            st[3] += __popcll(__ballot(busy != 0 && !wf_has_tri<TBL>(t) && t.cur != REF_NONE));
             st[7] += __popcll(__ballot(busy != 0 && (t.rid >> 30) == 2u));     // continuation-ray lane steps
             {   // steps whose fetch address is the same for every active lane
                 const uint64_t act = __ballot(busy != 0);
-                const uint32_t fo = t.lc > 0 ? 0x80000000u + (uint32_t)t.lt : t.cur;
+                const uint32_t fo = wf_has_tri<TBL>(t) ? 0x80000000u + (uint32_t)(t.lt & 0xffffff) : t.cur;
                 const uint32_t f0 = __shfl(fo, act ? __ffsll((long long)act) - 1 : 0);
                 st[4] += (act != 0 && __ballot(busy != 0 && fo != f0) == 0) ? 1 : 0;
             }
@@ -1008,11 +1042,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (done) {
                 const uint32_t kind = t.rid >> 30, p = t.rid & 0x3fffffffu;
                 if (!WF_DIAG_NOSTORE) {
-                    if (kind == 2) b.hit[p] = t.hitTri;
-                    else b.occ[2 * (size_t)p + kind] = t.hitTri >= 0 ? 1 : 0;
+                    if (kind == 2) b.hit[p] = wf_tri_index<TBL>(t.hitTri);
+                    else b.occ[2 * (size_t)p + kind] = t.hitTri != -1 ? 1 : 0;
                 }
                 busy = 0;
-                t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;     // (an any-hit ray may stop mid-tree)
+                t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;     // (an any-hit ray may stop mid-tree)
             }
         }
 #if WF_DIAG_VALU
@@ -1055,7 +1089,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
                                  s.root_max[2], zlo)) {
                         root = s.root_ref;
-                        if (root & REF_LEAF) { decode_leaf(s, root, nlt, nlc); root = REF_NONE; }
+                        if (root & REF_LEAF) { if (TBL) decode_leaf(s, root, nlt, nlc); else nlt = (int)root; root = REF_NONE; }
                     }
                     t.r = nr; t.tMax = ntmax; t.rid = (kind << 30) | p;
                     t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
@@ -1156,9 +1190,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_w
         if (mine && box_fast(t.r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
                              s.root_max[2], zlo)) {
             t.cur = s.root_ref;
-            if (t.cur & REF_LEAF) { decode_leaf(s, t.cur, t.lt, t.lc); t.cur = REF_NONE; }
+            if (t.cur & REF_LEAF) { if (TBL) decode_leaf(s, t.cur, t.lt, t.lc); else t.lt = (int)t.cur; t.cur = REF_NONE; }
         }
-        int busy = mine && (t.cur != REF_NONE || t.lc > 0);
+        int busy = mine && (t.cur != REF_NONE || wf_has_tri<TBL>(t));
         auto run = [&](auto ident_tag) {
             constexpr bool ID = decltype(ident_tag)::value;
             for (;;) {
@@ -1170,8 +1204,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, PT_PRIM_WF_WAVES) pt_primary_w
         else run(std::false_type{});
         if (!mine) continue;
         float4 q0, q1, q2;
-        if (t.hitTri >= 0) {
-            Hit h = make_hit(s, t.r, t.hitTri);
+        if (t.hitTri != -1) {
+            Hit h = make_hit(s, t.r, wf_tri_index<TBL>(t.hitTri));
             f3 em = get_emissive(s, h.mat);
             q0 = make_float4(h.P.x, h.P.y, h.P.z, __int_as_float((h.mat & 0x00ffffff) | ((h.tex + 1) << 24)));
             q1 = make_float4(h.N.x, h.N.y, h.N.z, h.u);

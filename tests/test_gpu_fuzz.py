@@ -138,3 +138,24 @@ def test_coincident_triangles_table_leaf(pt, copies):
         pt.render(0, 3)
         got = pt.read_accum()
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), mode
+
+
+def test_nonfinite_box_disables_culling(pt):
+    """A BVH box with an infinite coordinate (a conservative bound: the tree stays
+    a valid BVH).  z-slab culling's proof needs finite boxes, so the library
+    traverses such a scene without culling; every mode still equals the oracle
+    bit for bit."""
+    import dataclasses
+    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL
+    cfg, _ = random_scene(7)
+    nd = cfg.packed.nodes.copy()
+    leaf = int(np.flatnonzero(nd[:, 7] == -1)[0])
+    nd[leaf, 5] = np.inf                     # the first leaf's box max z
+    cfg = dataclasses.replace(cfg, packed=dataclasses.replace(cfg.packed, nodes=nd))
+    ref, _ = pyoracle.Oracle(cfg).render(0, 3)
+    for mode in (TRAVERSE_ZCULL, TRAVERSE_EXACT, TRAVERSE_ZCULL | KERNEL_V1):
+        pt.load(cfg, mode)
+        pt.reset_accum()
+        pt.render(0, 3)
+        got = pt.read_accum()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), mode
