@@ -625,15 +625,31 @@ PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa, bool pop) 
     return e;
 }
 
-// BoundIntersect (:213-228) for traversal decisions.  fminf/fmaxf (v_min/v_max)
-// drop NaNs exactly like the oracle's min/max; the results only feed
+// BoundIntersect (:213-228) for traversal decisions.  v_min / v_max (IEEE
+// minNum / maxNum) drop NaNs exactly like the oracle's min/max; the results only feed
 // comparisons, where the sign of a zero cannot matter -> same booleans.
 // box_slabs takes the six slab distances (far x y z, near x y z) and returns the
 // box's z-slab lower end (zlo) in the triangle test's frame.
+// (v_min / v_max written out: the slab distances are products, never signalling
+// NaNs, so the IEEE-mode instructions are fminf / fmaxf here -- the compiler's
+// own fminf inserted a quieting v_max x, x on two of them every step)
+PN_DEV float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+PN_DEV float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+PN_DEV float vmin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+PN_DEV float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 template <bool IDENT = false>
 PN_DEV bool box_slabs(const RayP& r, float fx, float fy, float fz, float nx, float ny, float nz, float& zlo) {
-    float t1 = fminf(fmaxf(fx, nx), fminf(fmaxf(fy, ny), fmaxf(fz, nz)));
-    float t0 = fmaxf(fminf(fx, nx), fmaxf(fminf(fy, ny), fminf(fz, nz)));
+    const float zmin = vmin(fz, nz), zmax = vmax(fz, nz);
+    float t1 = vmin3(vmax(fx, nx), vmax(fy, ny), zmax);
+    float t0 = vmax3(vmin(fx, nx), vmin(fy, ny), zmin);
     const int kz = IDENT ? 2 : r.kz();
     float zf = kz == 2 ? fz : (kz == 0 ? fx : fy);
     float zn = kz == 2 ? nz : (kz == 0 ? nx : ny);
@@ -641,7 +657,7 @@ PN_DEV bool box_slabs(const RayP& r, float fx, float fy, float fz, float nx, flo
     // distances are never NaN (finite ray, |d_kz| >= 1e-12, finite boxes: the
     // host disables culling otherwise), so min / max equal the compare-selects
     // of pt_kernel.h box_test -- and for kz = 2 they are the t0 / t1 terms above
-    float lo = fminf(zn, zf), hi = fmaxf(zn, zf);
+    float lo = IDENT ? zmin : vmin(zn, zf), hi = IDENT ? zmax : vmax(zn, zf);
     zlo = lo;
     // zhi <= 0: the whole box is behind the ray in the triangle test's frame
     return (t1 >= t0) & !(r.cull_ok() & (hi <= 0.0f));
@@ -760,21 +776,24 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     const bool both = hL & hR;
     wf_push<STK>(lds, b, t.spa, both, farRef, zFar);
     const uint32_t go = (hR & (!hL | rightFirst)) ? m.y : (hL ? m.x : REF_NONE);
-    const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
     if (TBL) {
+        const bool goLeaf = (go != REF_NONE) & ((go & REF_LEAF) != 0u);
         int gs, gc;
         decode_leaf_fast<TBL>(s, go, gs, gc);
         t.lt = goLeaf ? gs : t.lt;
         t.lc = goLeaf ? gc : t.lc;
     } else {
-        t.lt = goLeaf ? (int)go : t.lt;
+        t.lt = ((go != REF_NONE) & ((go & REF_LEAF) != 0u)) ? (int)go : t.lt;
     }
-    t.cur = isNode ? (goLeaf ? REF_NONE : go) : t.cur;
+    // a leaf or REF_NONE (both negative as int) -> REF_NONE, a node index stays;
+    // lanes that are no node lane keep REF_NONE (go is REF_NONE for them)
+    t.cur = (uint32_t)max((int)go, -1);
     // ---- next fetch target: pop when nothing is pending
     const bool idle = !done & !wf_has_tri<TBL>(t) & (t.cur == REF_NONE);
-    done = done | (idle & (t.spa < WF_SPA_STRIDE));
+    const bool stacked = t.spa >= WF_SPA_STRIDE;
+    done = done | (idle & !stacked);
     {
-        const bool pop = idle & (t.spa >= WF_SPA_STRIDE);
+        const bool pop = idle & stacked;
         const uint2 e = wf_pop<STK>(lds, b, t.spa, pop);
         const float z = __uint_as_float(e.y);
         const bool take = pop & !(cull & (z > zc));     // (zc: tMax after this step's acceptance, as before)
@@ -784,10 +803,13 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
             decode_leaf_fast<TBL>(s, pop ? e.x : REF_NONE, es, ec);   // (a non-popping lane's word may be stale: no table lookup)
             t.lt = (take & eLeaf) ? es : t.lt;
             t.lc = (take & eLeaf) ? ec : t.lc;
+            t.cur = (take & !eLeaf) ? e.x : t.cur;
         } else {
-            t.lt = (take & eLeaf) ? (int)e.x : t.lt;
+            // (as above: a popped node index reads as no pending triangle, a
+            // popped leaf becomes REF_NONE in cur)
+            t.lt = take ? (int)e.x : t.lt;
+            t.cur = take ? (uint32_t)max((int)e.x, -1) : t.cur;
         }
-        t.cur = (take & !eLeaf) ? e.x : t.cur;
     }
     return done;
 }
