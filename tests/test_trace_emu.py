@@ -1,0 +1,18 @@
+"""CPU model of the trace step's traversal state machine (tools/trace_emu.py):
+the packed pending-range word (REF_LEAF | count << 24 | first) and the wide
+first / count pair drive identical traversals -- same hits, same step counts --
+and the invariant the step relies on (pending triangles => cur == REF_NONE:
+the fourth-quarter fetch of a triangle lane lies out of range) holds at every
+step.  A model of the control flow in float64, not of the device bits."""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_packed_and_wide_ranges_agree():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "trace_emu.py"), "150"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
