@@ -10,7 +10,7 @@ while IFS= read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp --kernel-include-regex "${KREGEX:-pt_wf_trace}" -d gpurun_out/pmct/p${i} -o run \
-    --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmct/p${i}.log 2>&1
+    --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pmc > gpurun_out/pmct/p${i}.log 2>&1
   rc=$?; echo "pmc pass $i [$grp] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done <<GROUPS
 ${PMC_GROUPS}
