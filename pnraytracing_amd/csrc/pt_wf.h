@@ -222,6 +222,45 @@ PN_DEV uint32_t wf_block_rank(bool live, uint32_t& total) {
     total = tot;
     return base + lanes_below(m);
 }
+// The same compaction without a block barrier between the waves' loads: each
+// wave takes its range with one LDS atomic on the block's live-path counter
+// (zeroed by wf_live_init at the kernel's start), so a wave whose records have
+// arrived goes on to its next fetches instead of waiting for its block's slowest
+// wave.  Which range a wave gets depends on arrival order -- no result does: a
+// path's entry only names where its state, rays and trace results live.  The
+// block's total is read after wf_enqueue's first barrier.
+#ifndef WF_WAVE_RANK
+#define WF_WAVE_RANK 1
+#endif
+PN_DEV uint32_t* wf_live_ctr() {
+    __shared__ uint32_t c;
+    return &c;
+}
+#define WF_NBIN 8
+PN_DEV unsigned int (*wf_bins())[WF_NBIN + 1] {      // wf_enqueue's per-kind direction-bin counters
+    __shared__ unsigned int bin[3][WF_NBIN + 1];
+    return bin;
+}
+PN_DEV void wf_live_init() {
+    if (WF_WAVE_RANK) {
+        if (threadIdx.x == 0) *wf_live_ctr() = 0u;
+        if (WF_WAVE_RANK >= 2 && threadIdx.x < 3 * (WF_NBIN + 1)) (&wf_bins()[0][0])[threadIdx.x] = 0u;
+        __syncthreads();
+    }
+}
+PN_DEV uint32_t wf_wave_rank(bool live) {
+    const uint64_t m = __ballot(live);
+    uint32_t base = 0;
+    if ((threadIdx.x & 63) == 0 && m != 0)
+        base = __hip_atomic_fetch_add(wf_live_ctr(), (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(base) + lanes_below(m);
+}
+// A path's compacted entry within its block: the block-barrier rank, or the wave
+// rank (WF_WAVE_RANK; total is then filled in by wf_enqueue)
+PN_DEV uint32_t wf_entry_rank(bool live, uint32_t& total) {
+    if (WF_WAVE_RANK) { total = 0u; return wf_wave_rank(live); }
+    return wf_block_rank(live, total);
+}
 
 PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
     color = mk3(clampf(color.x, 0.f, 1.f), clampf(color.y, 0.f, 1.f), clampf(color.z, 0.f, 1.f));
@@ -448,7 +487,6 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
 #ifndef WF_SORT_OCTANT
 #define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
 #endif
-#define WF_NBIN 8
 PN_DEV int wf_dir_bin(const f3 d) {
     return WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
 }
@@ -467,10 +505,14 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
     // signs take the same near/far choice at every node (:448), so a wave walks
     // the tree more coherently.  Slots within a bin come from LDS atomics (order
     // not deterministic, which no result depends on).
-    __shared__ unsigned int bin[3][WF_NBIN + 1];
+    unsigned int (*bin)[WF_NBIN + 1] = wf_bins();
     const uint32_t need[3] = {WF_RLIGHT, WF_RENV, WF_RCONT};
-    for (int k = threadIdx.x; k < 3 * (WF_NBIN + 1); k += blockDim.x) (&bin[0][0])[k] = 0;
-    __syncthreads();
+    if (WF_WAVE_RANK < 2) {                 // (WF_WAVE_RANK 2: zeroed by wf_live_init)
+        for (int k = threadIdx.x; k < 3 * (WF_NBIN + 1); k += blockDim.x) (&bin[0][0])[k] = 0;
+        __syncthreads();
+        if (WF_WAVE_RANK) total = *wf_live_ctr();    // every wave counted its live paths before the barrier
+        if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
+    }
     int oct[3];
     unsigned int rank[3];
 #pragma unroll
@@ -481,6 +523,10 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
         rank[k] = (nfl & need[k]) ? atomicAdd(&bin[k][oct[k]], 1u) : 0u;
     }
     __syncthreads();
+    if (WF_WAVE_RANK >= 2) {
+        total = *wf_live_ctr();
+        if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
+    }
     if (threadIdx.x < 3) {
         const int k = threadIdx.x;
         if (WF_QUEUED(k)) {                   // exclusive prefix over the bins of a kind
@@ -517,6 +563,7 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
                                                        float4* colors) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     // path slot
     wf_reset_counters(b);
+    wf_live_init();
     bool cont = false;
     PathIn q;
     int x = 0, py = 0;
@@ -547,11 +594,10 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
         }
     }
     uint32_t total;
-    const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);    // compacted path entry
+    const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont, total);    // compacted path entry
     uint32_t nfl = 0;
     BounceRays rays;
     if (cont) nfl = wf_setup_core<WF_GEN_EARLY, (WF_SOBOL_PAIR & 2) != 0>(s, fp, b, j, i, 0, x, py, frame, q, rays);
-    if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
     wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
 }
 
@@ -676,6 +722,9 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
 #ifndef WF_BQ_PREFETCH
 #define WF_BQ_PREFETCH 0    // block queue: fetch the next segment when fewer rays than this remain (0 = off)
 #endif
+#ifndef WF_RAY_PF
+#define WF_RAY_PF 0         // ray-record prefetch distance in dequeue tickets (0 = off; see the trace kernel)
+#endif
 #ifndef WF_KIND_ORDER
 #define WF_KIND_ORDER 0x210 // sweep order of the ray kinds, one hex digit each (0 light, 1 env, 2 continuation)
 #endif
@@ -684,6 +733,27 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// WF_RAY_PF: the wave that dequeues a segment also pulls the ray records of the
+// segment its counter hands out WF_RAY_PF tickets later into the caches (one
+// dword per 64 B, LDS-DMA into a scratch area: no register holds it), so that
+// segment's refills read the Infinity Cache instead of HBM.  Wave-uniform.
+PN_DEV __attribute__((always_inline)) void wf_prefetch_rays(const WfBufs& b, uint32_t item, int lane) {
+    __shared__ uint32_t pf_sink[64];
+    const uint32_t sj = __builtin_amdgcn_readfirstlane(item / WF_NSUB);
+    const uint32_t qk = sj / b.nseg_k, j = sj - qk * b.nseg_k;
+    const uint32_t kind = (uint32_t)(WF_KIND_ORDER >> (4 * (2 - (int)qk))) & 0xfu;
+    const uint32_t e = j * 256u;               // the segment's 256 entries (< npad: every array holds npad)
+    const bool fromState = !WF_QUEUED(kind);
+    const float4* O = fromState ? b.wr.P0 + e : b.rayO + (size_t)wf_qidx((int)kind) * b.npad + e;
+    const float4* D = fromState ? (kind == 0 ? b.wr.P7 : b.wr.P1) + e : b.rayD + (size_t)wf_qidx((int)kind) * b.npad + e;
+    // (inline asm: the builtin's scalar-operand form failed instruction selection
+    // in this loop; an extra vector-memory op only makes the compiler's later
+    // vmcnt waits stricter, never looser)
+    const uint32_t sink = (uint32_t)(uintptr_t)pf_sink;
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, off\n\tglobal_load_lds_dword %1, off"
+                 :: "v"(O + lane * 4), "v"(D + lane * 4), "s"(__builtin_amdgcn_readfirstlane(sink)) : "m0", "memory");
 }
 
 // One lane's traversal state (a ray being traced).
@@ -893,6 +963,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     uint32_t witer = 0, witer_exh = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
 
+    auto prefetch_item = [&](uint32_t item) { if (item < nseg) wf_prefetch_rays(b, item, lane); };
     // dequeue the wave's next queue item into [next, end) / ckind, or set `exhausted`
     // (wave-uniform; lane 0 issues the atomic)
     auto dequeue = [&]() {
@@ -907,7 +978,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
             t = __builtin_amdgcn_readfirstlane(t);
             const uint32_t item = t * WF_QSHARDS + p;
-            if (item < nseg) { seg = item; break; }
+            if (item < nseg) {
+                seg = item;
+                if (WF_RAY_PF) prefetch_item((t + WF_RAY_PF) * WF_QSHARDS + p);
+                break;
+            }
             ++qpart;
         }
         if (seg >= nseg) { exhausted = true; if (WF_TIMING) { t_exh = __builtin_amdgcn_s_memrealtime(); witer_exh = witer; } }
@@ -1327,6 +1402,7 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
         if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = 0u;
         return;
     }
+    if (!FINAL) wf_live_init();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool cont = false;
     PathIn q;
@@ -1335,10 +1411,9 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     if (threadIdx.x < live) cont = wf_shade_path(s, fp, b, primary, colors, i, q, bounce, slot, x, py, frame);
     if (FINAL) return;                        // bounce + 1 == max_depth: cont is false for every path
     uint32_t total;
-    const uint32_t j = blockIdx.x * 256u + wf_block_rank(cont, total);
+    const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont, total);
     uint32_t nfl = 0;
     BounceRays rays;
     if (cont) nfl = wf_setup_core<WF_SHADE_EARLY, (WF_SOBOL_PAIR & 1) != 0>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
-    if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
     wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
 }
