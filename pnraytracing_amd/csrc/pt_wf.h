@@ -227,10 +227,15 @@ PN_DEV uint32_t wf_block_rank(bool live, uint32_t& total) {
 // (zeroed by wf_live_init at the kernel's start), so a wave whose records have
 // arrived goes on to its next fetches instead of waiting for its block's slowest
 // wave.  Which range a wave gets depends on arrival order -- no result does: a
-// path's entry only names where its state, rays and trace results live.  The
-// block's total is read after wf_enqueue's first barrier.
+// path's entry only names where its state, rays and trace results live.
+// WF_WAVE_RANK 1: the block's total is read after wf_enqueue's first barrier
+// (C2 shade -2.3 % against the block rank); 2: the same with one barrier less;
+// 3 (default): wf_enqueue without any barrier -- queued rays take their slots the
+// same way (one LDS atomic per wave, no direction-octant grouping: measured
+// neutral), and the last wave through writes the block's counts (shade another
+// -1.7 %, C2 +0.8 %, profiles/r03/s7/ab_enq_nobar_s15.txt).
 #ifndef WF_WAVE_RANK
-#define WF_WAVE_RANK 1
+#define WF_WAVE_RANK 3
 #endif
 PN_DEV uint32_t* wf_live_ctr() {
     __shared__ uint32_t c;
@@ -241,10 +246,15 @@ PN_DEV unsigned int (*wf_bins())[WF_NBIN + 1] {      // wf_enqueue's per-kind di
     __shared__ unsigned int bin[3][WF_NBIN + 1];
     return bin;
 }
+PN_DEV uint32_t* wf_enq_ctr() {     // WF_WAVE_RANK 3: queued rays per kind, waves through wf_enqueue
+    __shared__ uint32_t c[4];
+    return c;
+}
 PN_DEV void wf_live_init() {
     if (WF_WAVE_RANK) {
         if (threadIdx.x == 0) *wf_live_ctr() = 0u;
-        if (WF_WAVE_RANK >= 2 && threadIdx.x < 3 * (WF_NBIN + 1)) (&wf_bins()[0][0])[threadIdx.x] = 0u;
+        if (WF_WAVE_RANK == 2 && threadIdx.x < 3 * (WF_NBIN + 1)) (&wf_bins()[0][0])[threadIdx.x] = 0u;
+        if (WF_WAVE_RANK >= 3 && threadIdx.x < 4) wf_enq_ctr()[threadIdx.x] = 0u;
         __syncthreads();
     }
 }
@@ -507,6 +517,40 @@ PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRa
     // not deterministic, which no result depends on).
     unsigned int (*bin)[WF_NBIN + 1] = wf_bins();
     const uint32_t need[3] = {WF_RLIGHT, WF_RENV, WF_RCONT};
+    if (WF_WAVE_RANK >= 3) {
+        // no barrier: a queued kind's slots from one LDS atomic per wave (no octant
+        // grouping), and the wave that passes through here last writes the block's
+        // counts (its acquire sees every other wave's counter updates)
+        uint32_t* ec = wf_enq_ctr();
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (!WF_QUEUED(k)) continue;
+            const uint64_t m = __ballot((nfl & need[k]) != 0u);
+            uint32_t base = 0;
+            if (lane == 0 && m != 0)
+                base = __hip_atomic_fetch_add(ec + k, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (nfl & need[k]) {
+                const size_t slot = (size_t)wf_qidx(k) * b.npad + (size_t)blockIdx.x * 256 + base + lanes_below(m);
+                const f3 o = k == 1 ? rays.oP : rays.oOff;
+                const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
+                ps_st(b.rayO, slot, make_float4(o.x, o.y, o.z, __uint_as_float(i)));
+                ps_st(b.rayD, slot, make_float4(d.x, d.y, d.z, 0.f));
+            }
+        }
+        uint32_t done = 0;
+        if (lane == 0) done = __hip_atomic_fetch_add(ec + 3, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(done) == blockDim.x / 64 - 1) {
+            const uint32_t tot = __hip_atomic_load(wf_live_ctr(), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane < 3) {
+                const uint32_t qn = __hip_atomic_load(ec + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                b.segcount[lane * b.nseg_k + blockIdx.x] = WF_QUEUED(lane) ? qn : ((lane == 2 || lights) ? tot : 0u);
+            }
+            if (lane == 0) b.wr.bcount[blockIdx.x] = tot;
+        }
+        return;
+    }
     if (WF_WAVE_RANK < 2) {                 // (WF_WAVE_RANK 2: zeroed by wf_live_init)
         for (int k = threadIdx.x; k < 3 * (WF_NBIN + 1); k += blockDim.x) (&bin[0][0])[k] = 0;
         __syncthreads();
