@@ -84,8 +84,11 @@ def parse():
                     help="D configs: synchronise after every call (an interactive loop that displays each frame)")
     ap.add_argument("--mode", default="zcull", choices=["exact", "zcull"])
     ap.add_argument("--kernel", default="v3", choices=["v1", "v3"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample length")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="bounded CPU leg: the oracle renders parity row sets of the timed image for ~this long")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU leg's baseline timing (the parity check still renders one row set)")
+    ap.add_argument("--no-parity", action="store_true", help="skip the CPU leg entirely (no parity check)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes")
     ap.add_argument("--pmc-timeout", type=int, default=240, help="seconds per PMC pass (killed after)")
     ap.add_argument("--serial-steps", type=int, default=2,
@@ -235,29 +238,69 @@ def host_cpus():
     return usable, {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota}
 
 
-def cpu_baseline(cfg, target_s: float):
-    """CPU oracle (the C restatement of ray_tracing.comp, OpenMP over rows) on
-    whole 1080p 4-spp iterations of the same workload until ~target_s, plus C1
-    (the reference's CPU-runnable config) at full size, on every CPU the process
-    may use (host_cpus); returns (dict, counters)."""
+PARITY_STEP = 36     # the parity check's row sets: every 36th row, offsets interleaved
+
+
+def parity_offsets(step: int = PARITY_STEP):
+    """Row offsets of the successive parity row sets: 0, step/2, step/4, 3 step/4, ...
+    (each set is every step-th row; the sets interleave, so any prefix of them
+    spreads over the whole frame)."""
+    out, k = [0], 1
+    while k < step:
+        out += [o for o in ((2 * j + 1) * step // (2 * k) for j in range(k)) if o not in out]
+        k *= 2
+    return out + [o for o in range(step) if o not in out]
+
+
+def cpu_leg(cfg, gpu_image, frames: int, target_s: float):
+    """The CPU leg: the oracle (oracle/pn_oracle.c, the C restatement of
+    ray_tracing.comp, OpenMP over rows, every CPU the process may use) renders row
+    sets of the TIMED image -- every PARITY_STEP-th row, frames 0 .. frames-1 in
+    order, exactly what the GPU accumulated over the warm-up and the timed steps --
+    until ~target_s (at least one set).  Its rate is the CPU baseline (a bounded
+    sample of the same workload), and its rows are compared bit for bit with the
+    GPU's image: the parity of the measured run itself (ray_tracing.comp:975-991).
+    Returns (parity dict, cpu dict, counters)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle
-    from pnraytracing_amd import scenes
     threads, cpu_facts = host_cpus()
     o = pyoracle.Oracle(cfg)
-    H = cfg.height
-    acc = np.zeros((H, cfg.width, 4), np.float32)
-    tot = None
-    it = 0
+    H, W = cfg.height, cfg.width
+    ref = np.zeros((H, W, 4), np.float32)
+    tot, rows = None, []
     t = time.perf_counter()
-    while it < 8:
-        _, st = o.render(it * cfg.spp, cfg.spp, accum=acc, threads=threads)
+    for off in parity_offsets():
+        if off >= H:
+            continue
+        _, st = o.render(0, frames, rows=(off, H), y_step=PARITY_STEP, accum=ref, threads=threads)
         tot = st if tot is None else {k: tot[k] + st[k] for k in st}
-        it += 1
+        rows += list(range(off, H, PARITY_STEP))
         if time.perf_counter() - t >= target_s:
             break
     dt = time.perf_counter() - t
+    rows = np.array(sorted(rows))
+    g, r = gpu_image[rows].view(np.uint32), ref[rows].view(np.uint32)
+    bad = np.argwhere(np.any(g != r, axis=-1))
+    parity = {"rows": int(len(rows)), "row_step": PARITY_STEP, "pixels": int(len(rows) * W), "frames": frames,
+              "differing": int(len(bad)), "tolerance": "0 ulp (bit-exact)",
+              "oracle": "oracle/pn_oracle.c on the same scene arrays",
+              "first_differing": ([int(rows[bad[0][0]]), int(bad[0][1])] if len(bad) else None)}
     n = tot["samples"]
+    cpu = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "sample": f"{cfg.name}: {len(rows)} rows (every {PARITY_STEP}th, interleaved sets) x {W} px x {frames} frames "
+                     f"= {n} samples in {dt:.1f}s -- the parity rows of the timed image; oracle/pn_oracle.c "
+                     f"OpenMP {threads} threads",
+           "cpu_model": cpu_model(), **cpu_facts}
+    return parity, cpu, tot
+
+
+def cpu_baseline_c1(cpu: dict):
+    """C1 (the reference's CPU-runnable config, BASELINE configs[0]) at full size
+    on the same threads, added to the CPU leg's record."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    from pnraytracing_amd import scenes
+    threads = cpu["cores"]
     # C1: Cornell box, 256x256, 1 spp per frame, depth 4 (BASELINE configs[0]); frames until ~1 s
     c1 = scenes.cornell_c1()
     o1 = pyoracle.Oracle(c1)
@@ -267,13 +310,8 @@ def cpu_baseline(cfg, target_s: float):
         o1.render(f1, 1, accum=a1, threads=threads)
         f1 += 1
     d1 = time.perf_counter() - t1
-    cpu = {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-           "sample": f"{cfg.name}: {it} full {cfg.width}x{H} iterations x {cfg.spp} spp = {n} samples "
-                     f"in {dt:.1f}s, oracle/pn_oracle.c OpenMP {threads} threads",
-           "cpu_model": cpu_model(), **cpu_facts,
-           "c1": {"value": round(f1 * c1.width * c1.height / d1 / 1e6, 4), "unit": "Msamples/s",
-                  "sample": f"C1 256x256 x {f1} frames (1 spp each, depth 4) in {d1:.2f}s"}}
-    return cpu, tot
+    cpu["c1"] = {"value": round(f1 * c1.width * c1.height / d1 / 1e6, 4), "unit": "Msamples/s",
+                 "sample": f"C1 256x256 x {f1} frames (1 spp each, depth 4) in {d1:.2f}s"}
 
 
 def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26) -> int:
@@ -327,27 +365,45 @@ def same_on_all_ranks(values, device) -> None:
 
 
 def launches_per_step_of(k_launches: int, steps: int, excl: dict, kname: str):
-    """Dominant-kernel launches per step: from the timed region's events, else from
-    the PNRT_SERIAL steps (same call sizes), else unknown (None)."""
-    if k_launches:
-        return k_launches / steps
+    """Dominant-kernel launches per step, counted at the call size kernel_ms was
+    measured on: from the PNRT_SERIAL steps (whole calls of iters_per_call
+    iterations, as kernel_ms), else from the timed region's events, else unknown
+    (None).  (A timed region shorter than one call -- steps < iters_per_call --
+    issues shorter calls, whose launches are not the serial steps' launches.)"""
     if kname in excl and excl[kname].get("launches_per_step"):
         return excl[kname]["launches_per_step"]
+    if k_launches:
+        return k_launches / steps
     return None
 
 
-def derive_bound(hbm_frac, l2_hit, l2_frac):
+def derive_bound(hbm_frac, l2_hit, l2_frac, gather_hit=None):
     """The roof that binds, from the counters: "hbm" (bandwidth) when the kernel's
     fabric traffic reaches half the HBM peak; below that the kernel is bound by
-    the latency of its dependent fetch chains -- "hbm-latency" when most of its L2
-    lookups miss (a scene beyond the L2s: C5), "l2-latency" when they hit (C2:
-    L1/L2-hit chains).  l2_frac (its own requests against
-    the L2 bandwidth) is reported beside it."""
+    the latency of its dependent fetch chains -- "hbm-latency" when most of its
+    node / triangle gathers miss the L2 (a scene beyond the L2s: C5), "l2-latency"
+    when they hit (C2: L1/L2-hit chains).  The gathers' own
+    hit rate (gather_hit: the streamed ray records, read once, miss by nature and
+    are taken out) decides when known, else the kernel's whole L2 hit rate.
+    l2_frac (its own requests against the L2 bandwidth) is reported beside it."""
     if hbm_frac is None:
         return None
     if hbm_frac >= 0.5:
         return "hbm"
-    return "hbm-latency" if (l2_hit is not None and l2_hit < 0.6) else "l2-latency"
+    hit = gather_hit if gather_hit is not None else l2_hit
+    return "hbm-latency" if (hit is not None and hit < 0.6) else "l2-latency"
+
+
+def gather_hit_rate(fetch_bytes, streamed_bytes, requested_bytes, rays):
+    """L2 hit rate of the trace kernel's node / triangle gathers alone, in bytes:
+    1 - (fabric read bytes of the gathers) / (bytes the gathers requested).  The
+    gathers' fabric bytes are FETCH_SIZE less the streamed ray records' share
+    (tallied at half, CALIBRATION); their requests are the census's request
+    stream less the ray records (32 B + the 4-B path entry per ray)."""
+    req = requested_bytes - 36.0 * rays
+    if req <= 0:
+        return None
+    return max(0.0, min(1.0, 1.0 - (fetch_bytes - streamed_bytes / 2.0) / req))
 
 
 def main():
@@ -475,9 +531,13 @@ def main():
     k_ms_total, k_launches = prof.get(kname, (0.0, 0))
     kern_ms_pipe = k_ms_total / k_launches if k_launches else None   # average launch duration, pipelined
 
+    # the timed image itself (frames 0 .. (warmup + steps) * spp - 1), for the parity
+    # check of the CPU leg below; read before the PNRT_SERIAL steps add frames to it
+    timed_image = None
+    if rank == 0 and (args.save_image or not args.no_parity):
+        timed_image = image.cpu().numpy() if world > 1 else pt.read_accum()
     if args.save_image and rank == 0:
-        img = (image.cpu().numpy() if world > 1 else pt.read_accum())
-        np.save(args.save_image, img)
+        np.save(args.save_image, timed_image)
 
     # exclusive kernel times: PNRT_SERIAL steps (one call in flight, full trace grid)
     excl = {}
@@ -517,10 +577,19 @@ def main():
             setup["bvh_build_gpu_s"] = round(time.perf_counter() - t, 4)
             setup["bvh_gpu_identical"] = bool(np.array_equal(nodes.view(np.uint32), cfg.packed.nodes.view(np.uint32)))
 
-        cpu = None
-        counts = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu, counts = cpu_baseline(cfg, args.cpu_seconds)
+        cpu = counts = parity = None
+        if not args.no_parity:
+            # the CPU leg (rank 0): oracle rows of the timed image -- its parity, and at
+            # N = 1 the CPU baseline; N > 1 checks one row set (the gathered image)
+            timing = world == 1 and not args.no_cpu_baseline
+            parity, cpu, counts = cpu_leg(cfg, timed_image, (args.warmup + args.steps) * spp,
+                                          args.cpu_seconds if timing else 0.0)
+            if timing:
+                cpu_baseline_c1(cpu)
+            else:
+                cpu = None
+            log(f"parity: {parity['differing']} of {parity['pixels']} pixels differ "
+                f"({parity['rows']} rows x {parity['frames']} frames vs the oracle)")
         rows0 = sf.my_rows
         samples_per_step = rows0 * W * spp
         src_hash = build.device_source_hash()
@@ -532,7 +601,7 @@ def main():
                    else pyoracle.algorithmic_bytes(counts)) / counts["samples"]
             ref_bytes = round(per * samples_per_step / launches_per_step)
 
-        traffic = l2hit = None
+        traffic = l2hit = ghit = None
         traffic_src = None
         step_traffic = None
         census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
@@ -548,6 +617,8 @@ def main():
                 rays = sum(b["rays"] for b in census["per_bounce"]) / census["trace_launches"] * census_scale
                 streamed = min(32.0 * rays, e["fetch_bytes"] * STREAM_FACTOR)
                 traffic = e["fetch_bytes"] * GATHER_FACTOR + streamed / 2.0 + e["write_bytes"]
+                ghit = gather_hit_rate(e["fetch_bytes"], streamed, census["requested_bytes_per_launch"] * census_scale,
+                                       rays)
                 traffic_src = (f"live rocprofv3 --pmc: FETCH_SIZE + streamed ray bytes / 2 + WRITE_SIZE -- 64-B gathers "
                                f"tallied exactly, streamed reads at half ({CALIBRATION}); {rays / 1e6:.1f}M rays x 32 B "
                                f"per launch from profiles/census.json")
@@ -605,16 +676,18 @@ def main():
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
                        "kernel": kfull},
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
-                                               requested["frac_of_l2"] if requested else None),
+                                               requested["frac_of_l2"] if requested else None, ghit),
                          "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "
-                                       "else the latency of dependent fetch chains -- hbm-latency if l2_hit_rate < 0.6, "
-                                       "l2-latency otherwise; peak / frac stay against HBM",
+                                       "else the latency of dependent fetch chains -- hbm-latency if the node / "
+                                       "triangle gathers' L2 hit rate (gather_l2_hit_rate; l2_hit_rate when unknown) "
+                                       "< 0.6, l2-latency otherwise; peak / frac stay against HBM",
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": round(traffic) if traffic else None, "traffic_source": traffic_src,
                          "traffic_bounds": traffic_bounds,
                          "l2_hit_rate": round(l2hit, 4) if l2hit is not None else None,
+                         "gather_l2_hit_rate": round(ghit, 4) if ghit is not None else None,
                          "kernel": kfull, "kernel_ms": kern_ms, "kernel_ms_timing": "exclusive (PNRT_SERIAL steps)",
                          "kernel_ms_pipelined": round(kern_ms_pipe, 4) if kern_ms_pipe else None,
                          "launches_per_step": launches_per_step,
@@ -625,15 +698,20 @@ def main():
             "kernels_exclusive": excl or None,
             "fabric_traffic": step_traffic,
             "setup": setup,
+            "parity": parity,
             "cpu_baseline": cpu,
             "device": {"bvh_interior_nodes": info["n_interior"], "max_depth": info["max_depth"],
                        "scene_bytes": info["device_bytes"], "library": version},
         }
         print(json.dumps(line), flush=True)
+    failed = bool(parity and parity["differing"])
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     pt.close()
+    if failed:
+        log("PARITY FAILURE: the timed image differs from the oracle")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -90,6 +90,16 @@ int pnrt_upload_scene(pnrt_ctx* ctx,
                       const float* bvh_nodes, int n_nodes,
                       const float* lights, int n_lights, float lights_sum_area);
 
+/* Replaces the material panel's in-place edit of the material texture
+ * (include/ImGuiLayer.hpp:73-83: glTexSubImage1D on unit 1 when a slider
+ * moves, followed by main.cpp:592-596's redraw): overwrite materials
+ * first .. first + count - 1 with count records of 18 floats in the
+ * main.cpp:438-456 layout, without re-uploading or re-laying out the scene.
+ * Calls already issued render with the old records (the call waits for them);
+ * later calls see the new ones.  The caller resets the accumulation as the
+ * reference's redraw does (pnrt_reset_accum). */
+int pnrt_update_materials(pnrt_ctx* ctx, int first, int count, const float* materials18);
+
 /* Replaces the albedo texture uploads (main.cpp:527-554, units 5..24):
  * tightly packed 8-bit rows as stbi_load returns them; GL's default
  * UNPACK_ALIGNMENT of 4 is applied as glTexImage2D would. slot 0..19. */
@@ -128,8 +138,8 @@ int pnrt_set_options(pnrt_ctx* ctx, int options);
 int pnrt_render(pnrt_ctx* ctx, uint32_t first_frame, uint32_t n_frames, int band_rows,
                 int n_shards, int shard);
 
-/* Redraw semantics (main.cpp:592-596): zero the accumulation image.  Also
- * clears a PNRT_E_TRACE fault (it waits for the calls in flight first). */
+/* Redraw semantics (main.cpp:592-596): zero the accumulation image.  Waits
+ * for the calls in flight first, and clears a PNRT_E_TRACE fault. */
 int pnrt_reset_accum(pnrt_ctx* ctx);
 /* Synchronise and copy the width*height*4 floats (row 0 = bottom) to host. */
 int pnrt_read_accum(pnrt_ctx* ctx, float* rgba_out);

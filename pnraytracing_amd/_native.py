@@ -131,6 +131,7 @@ def _type_device(lib):
     _sig(lib, "pnrt_set_stream", INT, P, P)
     _sig(lib, "pnrt_upload_scene", INT, P, F, INT, F, INT, F, INT, F, INT, F, INT, ctypes.c_float)
     _sig(lib, "pnrt_upload_texture", INT, P, INT, U8, INT, INT, INT)
+    _sig(lib, "pnrt_update_materials", INT, P, INT, INT, F)
     _sig(lib, "pnrt_upload_env", INT, P, F, F, INT, INT)
     _sig(lib, "pnrt_set_frame", INT, P, INT, INT, ctypes.POINTER(Camera), INT)
     _sig(lib, "pnrt_set_options", INT, P, INT)

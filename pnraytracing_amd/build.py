@@ -79,7 +79,10 @@ def build_device(force=False, extra=()):
 # never the product library (pnrt_version() says DIAGNOSTIC BUILD).
 #   guard1  the trace kernel's block-queue claim gives up after one attempt, so
 #           queued rays go untraced: pnrt_* must report PNRT_E_TRACE
-DIAG_VARIANTS = {"guard1": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_GUARD=1"]}
+#   bounds  every fetch / store index of the integrator kernels checked against its
+#           array (pt_diag.h WF_DIAG_BOUNDS): a violation is reported as PNRT_E_TRACE
+DIAG_VARIANTS = {"guard1": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_GUARD=1"],
+                 "bounds": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_BOUNDS=1"]}
 
 
 def variant_path(name: str) -> str:

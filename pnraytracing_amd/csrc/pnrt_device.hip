@@ -73,6 +73,7 @@ struct pnrt_ctx {
     bool has_scene = false;
     int max_depth = 0, n_interior = 0, root_is_leaf = 0;
     int64_t scene_bytes = 0;
+    std::vector<int> light_mat;            // material of each light record's triangle (pnrt_update_materials)
     // env + textures
     void* hdr = nullptr;
     void* rnd = nullptr;
@@ -94,7 +95,7 @@ struct pnrt_ctx {
     // first WF_PIPES_LARGE of them, or all WF_PIPES for small calls (a multi-GPU
     // rank's share: its kernels are short, so a fourth call in flight fills the
     // gaps of the other three's dependent chains; measured at N = 8).  A pipe is its own
-    // worker stream(s) and primary / colour / path buffers, so call k+1 starts
+    // worker stream and primary / colour / path buffers, so call k+1 starts
     // while call k's kernels drain (one call's kernels fill the CUs the other's
     // trace kernel leaves idle while its last rays drain).  Only the blends are
     // ordered: they run in call order on the context stream, which therefore
@@ -103,18 +104,31 @@ struct pnrt_ctx {
     // (GPU_MAX_HW_QUEUES, HIP's default 4): with 4, its worker would share the
     // context stream's queue and serialise behind the blends, so small calls
     // rotate over the first three like large ones (n_pipes_small).
+    // (Splitting a call into two concurrent half-batches on two worker streams
+    // as well measured slower: 1 006 vs 1 105 Msamples/s.)
+    struct PrimKey {        // what a pipe's primary records were traced for (render_wavefront)
+        uint64_t epoch = 0; // scene_epoch at the time
+        float cam[12] = {};
+        int width = 0, height = 0, rows = 0, band = 0, n_shards = 0, shard = 0, mode = -1;
+        bool valid = false;
+    };
     struct Pipe {
-        hipStream_t w[2] = {nullptr, nullptr};
-        hipEvent_t ev_prim = nullptr, ev_join[2] = {nullptr, nullptr}, ev_blend = nullptr;
+        hipStream_t w = nullptr;
+        hipEvent_t ev_join = nullptr, ev_blend = nullptr;
         float4* primary = nullptr;  size_t primary_cap = 0;
+        PrimKey prim;
         float4* colors = nullptr;   size_t colors_cap = 0;
         void* wf = nullptr;         size_t wf_cap = 0;
-        uint2* ovf[2] = {nullptr, nullptr};
-        size_t ovf_cap[2] = {0, 0};
+        uint2* ovf = nullptr;       size_t ovf_cap = 0;
         bool blend_pending = false;  // ev_blend guards the colour buffer's last reader
     };
     Pipe pipe[WF_PIPES];
     unsigned n_pipes_small = WF_PIPES;     // pipes small calls rotate over (pipes_init)
+    unsigned last_pipe = 0;                // the pipe of the last call
+    // bumped by every change of what the primary records depend on besides the
+    // frame (camera, size, shard, traversal mode: compared per call): the scene
+    // arrays, the materials (emission) and the environment (a miss's colour)
+    uint64_t scene_epoch = 1;
     hipEvent_t ev_last = nullptr;          // recorded after every op the context queues on `stream`, so a
     bool last_valid = false;               // pnrt_set_stream orders the new stream after it without
                                            // touching the old stream (which the caller may have destroyed)
@@ -143,10 +157,18 @@ static int check_fault(pnrt_ctx* c) {
         static const char* what[WF_FAULT_WORDS] = {
             "a bounded wait of the trace kernel's block ray queue ran out",
             "a trace block loaded fewer rays than it dequeued",
-            "a trace launch ended with ray-queue items never dequeued", "?"};
+            "a trace launch ended with ray-queue items never dequeued",
+            "diagnostic bounds check: a fetch / store index out of range at site "};
+        static const char* site[] = {"?", "node", "triangle", "leaf table", "stack spill", "trace result", "ray record",
+                                     "hit attributes", "light record", "env footprint", "albedo texel", "primary record",
+                                     "colour", "path state", "segment"};
         std::string m;
-        for (int k = 0; k < WF_FAULT_WORDS; ++k)
-            if (__atomic_load_n(c->fault_host + k, __ATOMIC_ACQUIRE)) m += (m.empty() ? "" : "; ") + std::string(what[k]);
+        for (int k = 0; k < WF_FAULT_WORDS; ++k) {
+            const uint32_t v = __atomic_load_n(c->fault_host + k, __ATOMIC_ACQUIRE);
+            if (!v) continue;
+            m += (m.empty() ? "" : "; ") + std::string(what[k]);
+            if (k == WF_FAULT_BOUNDS) m += std::string(v < sizeof site / sizeof *site ? site[v] : "?") + " (" + std::to_string(v) + ")";
+        }
         if (!m.empty()) {
             c->faulted = true;
             c->fault_msg = "trace fault: " + m + " -- queued rays may be untraced, the accumulation image is "
@@ -170,12 +192,11 @@ static int mark_stream(pnrt_ctx* c) {
     return PNRT_OK;
 }
 
-// every stream the context launches on (user-visible stream, blend stream, workers)
+// every stream the context launches on (the caller's / blend stream, the workers)
 static hipError_t sync_all(pnrt_ctx* c) {
     hipError_t e = hipStreamSynchronize(c->stream);
     for (auto& P : c->pipe)
-        for (hipStream_t w : P.w)
-            if (e == hipSuccess && w) e = hipStreamSynchronize(w);
+        if (e == hipSuccess && P.w) e = hipStreamSynchronize(P.w);
     return e;
 }
 
@@ -266,11 +287,13 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #define WF_TRACE_PATHS_PER_BLOCK_ALONE WF_TRACE_BLOCK  // ... for a call with no other call in flight
 #endif
 
-// Wavefront buffers of one batch of n path slots, carved from `base`.
+// Wavefront buffers of one batch of n path slots, carved from `base` (wf_layout):
+// two path-state sets (P0-P7 + block counts), hit / occ, the env ray records,
+// segment counts, dequeue counters + census words (+ the timing builds' stamps).
 static size_t wf_bytes(size_t n) {
-    const size_t npad = (n + 255) / 256 * 256;
-    return 2 * (npad * 16 * 7 + (npad / 256) * 4 + 256) + n * (4 + 2) + 256 + npad * 96 + (npad / 256) * 12 + 256 +
-           2048 + 256 + 512 + (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
+    const size_t npad = (n + 255) / 256 * 256, nseg = npad / 256;
+    return 2 * (npad * 16 * 8 + nseg * 4 + 256) + n * (4 + 2) + 256 + npad * 32 + nseg * 12 + 256 + 2048 + 512 +
+           (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
 }
 // The two path-state sets of a batch (entries are indexed up to npad: a block's
 // live paths are compacted to the front of its 256 entries).
@@ -286,7 +309,6 @@ static WfLayout wf_layout(char* base, size_t n) {
     for (PathSet& ps : L.set) {
         float4** f4[] = {&ps.P0, &ps.P1, &ps.P2, &ps.P3, &ps.P4, &ps.P5, &ps.P6, &ps.P7};
         for (float4** q : f4) {
-            if (q == &ps.P7 && !WF_LIGHT_FROM_STATE) { *q = nullptr; continue; }
             *q = reinterpret_cast<float4*>(base + off); off += npad * 16;
         }
         ps.bcount = reinterpret_cast<uint32_t*>(base + off); off += (npad / 256) * 4;
@@ -299,8 +321,8 @@ static WfLayout wf_layout(char* base, size_t n) {
     off = (off + 255) & ~(size_t)255;
     b.npad = (uint32_t)((n + 255) / 256 * 256);
     b.nseg_k = b.npad / 256;
-    // ray records of the queued kinds (env; light / continuation unless traced from the state)
-    const size_t rec = (size_t)b.npad * 16 * WF_NQUEUED;
+    // ray records of the queued kind (env shadow rays; the others are traced from the state)
+    const size_t rec = (size_t)b.npad * 16;
     b.rayO = reinterpret_cast<float4*>(base + off); off += rec;
     b.rayD = reinterpret_cast<float4*>(base + off); off += rec;
     b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
@@ -325,6 +347,57 @@ static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false) 
     return ppb ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + ppb - 1) / ppb)) : (unsigned)gmax;
 }
 
+// WF_STATS / WF_TIMING builds: the trace launch's census / per-wave drain
+// timestamps, printed to stderr (tools/census.py, tools/trace_stats.py)
+static int report_trace_diag(pnrt_ctx* c, const WfBufs& b, hipStream_t st, int bounce, unsigned grid) {
+    if (WF_TIMING) {   // tail census: when the queue ran dry vs when the last wave ended
+        const size_t nw = (size_t)grid * (WF_TRACE_BLOCK / 64);   // waves launched
+        std::vector<unsigned long long> t(4 * nw);
+        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipMemcpy(t.data(), b.stats + 8, t.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, tex = ~0ull, tend = 0;
+        std::vector<unsigned long long> ends;
+        for (size_t w = 0; w < nw; ++w) {
+            t0 = std::min(t0, t[4 * w]);
+            if (t[4 * w + 1]) tex = std::min(tex, t[4 * w + 1]);
+            tend = std::max(tend, t[4 * w + 2]);
+            ends.push_back(t[4 * w + 2]);
+        }
+        std::sort(ends.begin(), ends.end());
+        auto us = [&](unsigned long long v) { return (double)(v - t0) / 100.0; };
+        fprintf(stderr, "[trace timing] bounce %d n=%u first-empty %.1f us, wave ends p10 %.1f p50 %.1f p90 %.1f "
+                "max %.1f us\n", bounce, b.n, us(tex), us(ends[nw / 10]), us(ends[nw / 2]), us(ends[nw * 9 / 10]),
+                us(tend));
+        // the slowest 1 % of waves: end time and their longest last ray (kind, lane steps)
+        std::vector<std::pair<unsigned long long, unsigned long long>> we;
+        for (size_t w = 0; w < nw; ++w) we.push_back({t[4 * w + 2], w});
+        std::sort(we.begin(), we.end());
+        fprintf(stderr, "[trace tail] bounce %d (end us, kind/lane steps of the last ray, iterations and us after the queue ran dry):", bounce);
+        for (size_t q = nw - std::max<size_t>(1, nw / 100); q < nw; q += std::max<size_t>(1, nw / 1000)) {
+            const size_t w = we[q].second;
+            const unsigned long long v = t[4 * w + 3];
+            fprintf(stderr, " %.0f:k%llu/%llu:%llu/%.0f", us(t[4 * w + 2]), (v >> 16) & 0xffff, v & 0xffff, v >> 32,
+                    (double)(t[4 * w + 2] - t[4 * w + 1]) / 100.0);
+        }
+        fprintf(stderr, "\n");
+    }
+    if (WF_STATS) {
+        unsigned long long stt[8 + 48];
+        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
+        for (int k = 0; k < 3; ++k) {        // lane steps per ray, log2 buckets, by ray kind
+            fprintf(stderr, "[trace hist] bounce %d kind %d:", bounce, k);
+            for (int q = 0; q < 16; ++q) fprintf(stderr, " %llu", stt[8 + 16 * k + q]);
+            fprintf(stderr, "\n");
+        }
+        fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu uniform-fetch iters=%llu "
+                "refills=%llu rays=%llu  lane-steps/ray=%.1f  continuation lane-steps=%.1f%%\n", bounce, b.n, stt[0],
+                stt[0] ? (double)stt[1] / stt[0] : 0.0, stt[2], stt[3], stt[4], stt[5], stt[6],
+                stt[6] ? (double)stt[1] / stt[6] : 0.0, stt[1] ? 100.0 * stt[7] / stt[1] : 0.0);
+    }
+    return PNRT_OK;
+}
+
 // One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
 // its colours land in frame slots [0, cf) of `colors`.
 static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, const WfLayout& L, hipStream_t st,
@@ -338,64 +411,20 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
     }
     HIPCHK(c, hipGetLastError());
+    const unsigned tg = trace_grid_for(c, b.n, alone);
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
-        // segment dequeue counter (+ the WF_STATS census)
-        // (zeroed by the setup kernel that queued the rays; the census builds also memset)
+        // segment dequeue counters: zeroed by the setup kernel that queued the rays
+        // (the census builds also clear their words)
         if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
-            const dim3 g(trace_grid_for(c, b.n, alone));
             if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)
-                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false, true>), g, dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
-            else hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false, false>), g, dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
+                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
+            else hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
         }
         HIPCHK(c, hipGetLastError());
-        if (WF_TIMING) {   // tail census: when the queue ran dry vs when the last wave ended
-            const size_t nw = (size_t)trace_grid_for(c, b.n, alone) * (WF_TRACE_BLOCK / 64);   // waves launched
-            std::vector<unsigned long long> t(4 * nw);
-            HIPCHK(c, hipStreamSynchronize(st));
-            HIPCHK(c, hipMemcpy(t.data(), b.stats + 8, t.size() * 8, hipMemcpyDeviceToHost));
-            unsigned long long t0 = ~0ull, tex = ~0ull, tend = 0;
-            std::vector<unsigned long long> ends;
-            for (size_t w = 0; w < nw; ++w) {
-                t0 = std::min(t0, t[4 * w]);
-                if (t[4 * w + 1]) tex = std::min(tex, t[4 * w + 1]);
-                tend = std::max(tend, t[4 * w + 2]);
-                ends.push_back(t[4 * w + 2]);
-            }
-            std::sort(ends.begin(), ends.end());
-            auto us = [&](unsigned long long v) { return (double)(v - t0) / 100.0; };
-            fprintf(stderr, "[trace timing] bounce %d n=%u first-empty %.1f us, wave ends p10 %.1f p50 %.1f p90 %.1f "
-                    "max %.1f us\n", bounce, b.n, us(tex), us(ends[nw / 10]), us(ends[nw / 2]), us(ends[nw * 9 / 10]),
-                    us(tend));
-            // the slowest 1 % of waves: end time and their longest last ray (kind, lane steps)
-            std::vector<std::pair<unsigned long long, unsigned long long>> we;
-            std::vector<unsigned long long> wx;
-            for (size_t w = 0; w < nw; ++w) we.push_back({t[4 * w + 2], w});
-            std::sort(we.begin(), we.end());
-            fprintf(stderr, "[trace tail] bounce %d (end us, kind/lane steps of the last ray, iterations and us after the queue ran dry):", bounce);
-            for (size_t q = nw - std::max<size_t>(1, nw / 100); q < nw; q += std::max<size_t>(1, nw / 1000)) {
-                const size_t w = we[q].second;
-                const unsigned long long c = t[4 * w + 3];
-                fprintf(stderr, " %.0f:k%llu/%llu:%llu/%.0f", us(t[4 * w + 2]), (c >> 16) & 0xffff, c & 0xffff, c >> 32,
-                        (double)(t[4 * w + 2] - t[4 * w + 1]) / 100.0);
-            }
-            fprintf(stderr, "\n");
-        }
-        if (WF_STATS) {
-            unsigned long long stt[8 + 48];
-            HIPCHK(c, hipStreamSynchronize(st));
-            HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
-            for (int k = 0; k < 3; ++k) {        // lane steps per ray, log2 buckets, by ray kind
-                fprintf(stderr, "[trace hist] bounce %d kind %d:", bounce, k);
-                for (int q = 0; q < 16; ++q) fprintf(stderr, " %llu", stt[8 + 16 * k + q]);
-                fprintf(stderr, "\n");
-            }
-            fprintf(stderr, "[trace stats] bounce %d n=%u iters=%llu active/iter=%.1f tri=%llu node=%llu uniform-fetch iters=%llu "
-                    "refills=%llu rays=%llu  lane-steps/ray=%.1f  continuation lane-steps=%.1f%%\n", bounce, b.n, stt[0],
-                    stt[0] ? (double)stt[1] / stt[0] : 0.0, stt[2], stt[3], stt[4], stt[5], stt[6],
-                    stt[6] ? (double)stt[1] / stt[6] : 0.0, stt[1] ? 100.0 * stt[7] / stt[1] : 0.0);
-        }
+        if (WF_STATS || WF_TIMING)
+            if (int rc = report_trace_diag(c, b, st, bounce, tg)) return rc;
         {
             ProfScope ps(c, PNRT_K_SHADE, st);
             // MIS + continuation, then the next bounce's sampling (sets alternate)
@@ -419,19 +448,19 @@ static int pipes_init(pnrt_ctx* c) {
     c->n_pipes_small = hw_queues > 4 ? WF_PIPES : WF_PIPES_LARGE;
     for (unsigned i = 0; i < c->n_pipes_small; ++i) {
         auto& P = c->pipe[i];
-        for (int k = 0; k < (WF_SPLIT ? 2 : 1); ++k) HIPCHK(c, hipStreamCreateWithFlags(&P.w[k], hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&P.ev_prim, hipEventDisableTiming));
-        for (auto& e : P.ev_join) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(c, hipStreamCreateWithFlags(&P.w, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&P.ev_blend, hipEventDisableTiming));
     }
     return PNRT_OK;
 }
 
-// v3 wavefront, one pnrt_render call on the next pipe: primary pass, then per
-// group of <= 8 frames two half-batches (each gen -> {trace -> shade} x depth) on
-// the pipe's two worker streams, then the frame-ordered blend on the blend stream.
-// The halves and consecutive calls are independent path sets, so running them
-// concurrently changes nothing in the result; the blends keep frame order.
+// v3 wavefront, one pnrt_render call on a pipe: the primary pass (unless the
+// pipe's records are still valid, PrimKey), then per group of <= 16 frames one
+// batch (gen -> {trace -> shade} x depth) on the pipe's worker stream, then the
+// frame-ordered blend on the context stream.  Consecutive calls are independent
+// path sets, so running them concurrently changes nothing in the result; the
+// blends keep frame order.
 static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, uint32_t first, uint32_t nf) {
     int rc;
     if ((rc = pipes_init(c))) return rc;
@@ -454,92 +483,85 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
                         : call_paths < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small
                         : call_paths < (size_t)WF_HUGE_CALL_PATHS ? WF_PIPES_MEDIUM : WF_PIPES_LARGE;
     const unsigned npipes = std::max(1u, std::min(want, c->n_pipes_small));   // only sets pipes_init made
-    const unsigned pi = c->next_pipe % npipes;
-    c->next_pipe = (pi + 1) % npipes;
     // no other call in flight: every pipe's last blend (its last work) has completed
     bool alone = !c->serial;
     for (auto& Q : c->pipe)
         if (alone && Q.blend_pending && hipEventQuery(Q.ev_blend) != hipSuccess) alone = false;
+    // A call with nothing in flight stays on the last call's pipe (its buffers are
+    // free, its primary records likely still valid, its lines still in the caches);
+    // otherwise the calls rotate over the pipes
+    const unsigned pi = (alone && c->last_pipe < npipes) ? c->last_pipe : c->next_pipe % npipes;
+    c->next_pipe = (pi + 1) % npipes;
+    c->last_pipe = pi;
     pnrt_ctx::Pipe& P = c->pipe[pi];
     if (c->trace_grid == 0) {
         int per_cu = 0, cus = 0;
-        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false, false>, WF_TRACE_BLOCK, 0));
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false>, WF_TRACE_BLOCK, 0));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
     }
-    const bool split = WF_SPLIT && chunk >= 2;
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;
     const size_t ovf_bytes = (size_t)c->trace_grid * WF_TRACE_BLOCK * ovf_stride * 8;
-    const uint32_t cfA0 = split ? (chunk + 1) / 2 : chunk;
-    const size_t bytesA = wf_bytes(per_frame * cfA0), bytesB = split ? wf_bytes(per_frame * (chunk - cfA0)) : 0;
     // every buffer set this call size rotates over is sized now, so no later call of
     // the same size reallocates (a reallocation waits for all calls in flight)
     for (unsigned q = 0; q < npipes; ++q) {
         pnrt_ctx::Pipe& Q = c->pipe[(pi + q) % npipes];
+        const float4* old_primary = Q.primary;
         if ((rc = grow(c, (void**)&Q.primary, &Q.primary_cap, pix * 48)) ||
             (rc = grow(c, (void**)&Q.colors, &Q.colors_cap, pix * 16 * chunk)) ||
-            (rc = grow(c, &Q.wf, &Q.wf_cap, bytesA + bytesB + 512)) ||
-            (rc = grow(c, (void**)&Q.ovf[0], &Q.ovf_cap[0], ovf_bytes)) ||
-            (split && (rc = grow(c, (void**)&Q.ovf[1], &Q.ovf_cap[1], ovf_bytes))))
+            (rc = grow(c, &Q.wf, &Q.wf_cap, wf_bytes(per_frame * chunk) + 512)) ||
+            (rc = grow(c, (void**)&Q.ovf, &Q.ovf_cap, ovf_bytes)))
             return rc;
+        if (Q.primary != old_primary) Q.prim.valid = false;
     }
     ++c->ncall;
-    hipStream_t w0 = P.w[0], w1 = P.w[1] ? P.w[1] : P.w[0];
+    hipStream_t w = P.w;
     // this pipe's buffers were last read by the blend of the call that used it last
-    if (P.blend_pending) {
-        HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
-        if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));
-    }
-    {
-        ProfScope ps(c, PNRT_K_PRIMARY, w0);
-        if (PT_PRIM_WF) {     // the trace kernel's step, grid-stride, the call's first spill area
-            WfBufs pb{};
-            pb.ovf = P.ovf[0];
-            pb.ovf_stride = (uint32_t)ovf_stride;
-            const unsigned gp = (unsigned)std::min<size_t>((pix + WF_TRACE_BLOCK - 1) / WF_TRACE_BLOCK, (size_t)c->trace_grid);
-            if (s.has_leaf_table)
-                hipLaunchKernelGGL((pt_primary_wf<WF_STACK, true>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w0, s, fp, pb, P.primary);
-            else hipLaunchKernelGGL((pt_primary_wf<WF_STACK, false>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w0, s, fp, pb, P.primary);
-        } else {
-            hipLaunchKernelGGL(pt_primary_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, w0, s, fp, P.primary);
-        }
-    }
-    HIPCHK(c, hipGetLastError());
-    if (w1 != w0) {
-        HIPCHK(c, hipEventRecord(P.ev_prim, w0));
-        HIPCHK(c, hipStreamWaitEvent(w1, P.ev_prim, 0));
+    if (P.blend_pending) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));
+    // The primary records (camera ray's closest hit per pixel of the shard) depend
+    // on the camera, the frame size, the shard, the traversal mode and the scene
+    // (scene_epoch: arrays, materials, environment) -- not on the frame number: the
+    // camera ray has no jitter (ray_tracing.comp:205-211, 980).  A pipe whose
+    // records were traced for the same key reuses them (read-only since), exactly.
+    pnrt_ctx::PrimKey key;
+    key.epoch = c->scene_epoch;
+    std::memcpy(key.cam, fp.eye, 12); std::memcpy(key.cam + 3, fp.llc, 12);
+    std::memcpy(key.cam + 6, fp.hor, 12); std::memcpy(key.cam + 9, fp.ver, 12);
+    key.width = fp.width; key.height = fp.height; key.rows = fp.rows;
+    key.band = fp.band; key.n_shards = fp.n_shards; key.shard = fp.shard; key.mode = fp.mode;
+    key.valid = true;
+    const bool prim_hit = P.prim.valid && P.prim.epoch == key.epoch && !std::memcmp(P.prim.cam, key.cam, sizeof key.cam) &&
+                          P.prim.width == key.width && P.prim.height == key.height && P.prim.rows == key.rows &&
+                          P.prim.band == key.band && P.prim.n_shards == key.n_shards && P.prim.shard == key.shard &&
+                          P.prim.mode == key.mode;
+    if (!prim_hit) {
+        ProfScope ps(c, PNRT_K_PRIMARY, w);
+        // the trace kernel's step, grid-stride, the pipe's spill area
+        WfBufs pb{};
+        pb.ovf = P.ovf;
+        pb.fault = c->fault_dev;
+        pb.ovf_stride = (uint32_t)ovf_stride;
+        const unsigned gp = (unsigned)std::min<size_t>((pix + WF_TRACE_BLOCK - 1) / WF_TRACE_BLOCK, (size_t)c->trace_grid);
+        if (s.has_leaf_table)
+            hipLaunchKernelGGL((pt_primary_wf<WF_STACK, true>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w, s, fp, pb, P.primary);
+        else hipLaunchKernelGGL((pt_primary_wf<WF_STACK, false>), dim3(gp), dim3(WF_TRACE_BLOCK), 0, w, s, fp, pb, P.primary);
+        HIPCHK(c, hipGetLastError());
+        P.prim = key;
     }
     for (uint32_t f0 = 0; f0 < nf; f0 += chunk) {
         const uint32_t cf = (nf - f0) < chunk ? (nf - f0) : chunk;
-        const uint32_t cfA = split && cf >= 2 ? (cf + 1) / 2 : cf, cfB = cf - cfA;
-        char* base = static_cast<char*>(P.wf);
-        WfLayout a = wf_layout(base, per_frame * cfA);
-        a.b.ovf = P.ovf[0];
+        WfLayout a = wf_layout(static_cast<char*>(P.wf), per_frame * cf);
+        a.b.ovf = P.ovf;
         a.b.fault = c->fault_dev;
         a.b.ovf_stride = (uint32_t)ovf_stride;
-        a.b.chunk_frames = (int)cfA;
+        a.b.chunk_frames = (int)cf;
         a.b.tiles_x = tiles_x;
         a.b.first_frame = first + f0;
-        if (f0) {                        // the previous group's blend has read the colours
-            HIPCHK(c, hipStreamWaitEvent(w0, P.ev_blend, 0));
-            if (w1 != w0) HIPCHK(c, hipStreamWaitEvent(w1, P.ev_blend, 0));
-        }
-        if (cfB) {
-            WfLayout bb = wf_layout(base + ((bytesA + 255) & ~(size_t)255), per_frame * cfB);
-            bb.b.ovf = P.ovf[1];
-            bb.b.fault = c->fault_dev;
-            bb.b.ovf_stride = (uint32_t)ovf_stride;
-            bb.b.chunk_frames = (int)cfB;
-            bb.b.tiles_x = tiles_x;
-            bb.b.first_frame = first + f0 + cfA;
-            if ((rc = render_batch(c, s, fp, bb, w1, P.primary, P.colors + (size_t)cfA * pix, alone))) return rc;
-            HIPCHK(c, hipEventRecord(P.ev_join[1], w1));
-            HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[1], 0));
-        }
-        if ((rc = render_batch(c, s, fp, a, w0, P.primary, P.colors, alone))) return rc;
-        HIPCHK(c, hipEventRecord(P.ev_join[0], w0));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join[0], 0));
+        if (f0) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));   // the previous group's blend has read the colours
+        if ((rc = render_batch(c, s, fp, a, w, P.primary, P.colors, alone))) return rc;
+        HIPCHK(c, hipEventRecord(P.ev_join, w));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join, 0));
         {   // the blends run in call order on the caller's stream
             ProfScope ps(c, PNRT_K_BLEND);
             hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
@@ -626,11 +648,9 @@ void pnrt_destroy(pnrt_ctx* c) {
     (void)hipFree(c->accum);
     (void)sync_all(c);
     for (auto& P : c->pipe) {
-        (void)hipFree(P.primary); (void)hipFree(P.colors); (void)hipFree(P.wf);
-        for (uint2* o : P.ovf) (void)hipFree(o);
-        for (hipStream_t w : P.w) if (w) (void)hipStreamDestroy(w);
-        if (P.ev_prim) (void)hipEventDestroy(P.ev_prim);
-        for (hipEvent_t e : P.ev_join) if (e) (void)hipEventDestroy(e);
+        (void)hipFree(P.primary); (void)hipFree(P.colors); (void)hipFree(P.wf); (void)hipFree(P.ovf);
+        if (P.w) (void)hipStreamDestroy(P.w);
+        if (P.ev_join) (void)hipEventDestroy(P.ev_join);
         if (P.ev_blend) (void)hipEventDestroy(P.ev_blend);
     }
 
@@ -683,6 +703,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     HIPCHK(c, sync_all(c));
     free_scene(c);
     c->scene_bytes = 0;
+    ++c->scene_epoch;                    // primary records of the old scene are stale
 
     // triangles: positions gathered in BVH order, ids validated
     std::vector<float4> tris((size_t)nt * 3 + 1);   // +1: the trace kernel reads 64 B per record
@@ -801,6 +822,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     uint32_t root_ref = childref(0);
     const int has_leaf_table = packed ? 0 : 1;
     if (leaf_table.empty()) leaf_table.push_back(make_int2(0, 0));
+
     // trace-kernel stack bound: at most one deferred sibling per BVH level
     c->wf_stack_need = maxd + 2;
     std::vector<float2> lights(nl > WF_LIGHT_SCAN ? nl : WF_LIGHT_SCAN, make_float2(0.f, 0.f));
@@ -814,6 +836,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     // light entry k -- its triangle's vertex records and material emission -- in one
     // place; entry nl is triangle 0 (GetLightIndex's fallback index)
     std::vector<float4> lrec((size_t)(nl + 1) * 7);
+    c->light_mat.assign((size_t)nl + 1, 0);
     for (int e = 0; e <= nl; ++e) {
         const int t = e < nl ? fint(Lt[3 * (size_t)e]) : 0;
         for (int k = 0; k < 3; ++k) {
@@ -824,6 +847,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         const int mat = fint(T[6 * (size_t)t + 3]);
         const float* em = M + 18 * (size_t)mat;
         lrec[7 * (size_t)e + 6] = make_float4(em[0], em[1], em[2], 0.f);
+        c->light_mat[e] = mat;
     }
 
     DevScene& s = c->scene;
@@ -862,6 +886,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
             if (!std::isfinite(N[12 * i + k])) { c->boxes_finite = false; break; }
     s.root_ref = root_ref;
     s.has_leaf_table = has_leaf_table;
+    s.n_leaf_table = (int)leaf_table.size();
     {   // GetLightIndex is a lower bound: a linear scan returns the same index iff the
         // prefix areas are non-decreasing (they are for main.cpp:374-383's list)
         bool mono = nl <= WF_LIGHT_SCAN;
@@ -874,6 +899,30 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
     c->n_interior = (int)order.size();
     c->max_depth = maxd;
     c->has_scene = true;
+    return PNRT_OK;
+}
+
+int pnrt_update_materials(pnrt_ctx* c, int first, int count, const float* rec) {
+    if (!c) return PNRT_E_ARG;
+    if (!c->has_scene) return set_err(c, PNRT_E_STATE, "update_materials: upload_scene first");
+    if (first < 0 || count < 0 || first > c->scene.n_materials - count || (count > 0 && !rec))
+        return set_err(c, PNRT_E_ARG, "update_materials: material range outside the uploaded array");
+    if (count == 0) return PNRT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    // the calls in flight render with the old records (the reference's
+    // glTexSubImage1D is ordered after the dispatches issued before it)
+    HIPCHK(c, sync_all(c));
+    HIPCHK(c, hipMemcpy(const_cast<float*>(c->scene.materials) + 18 * (size_t)first, rec, 18 * sizeof(float) * (size_t)count,
+                        hipMemcpyHostToDevice));
+    // light records carry a copy of their triangle's emission (upload_scene)
+    for (size_t e = 0; e < c->light_mat.size(); ++e) {
+        const int m = c->light_mat[e];
+        if (m < first || m >= first + count) continue;
+        const float* em = rec + 18 * (size_t)(m - first);
+        const float4 v = make_float4(em[0], em[1], em[2], 0.f);
+        HIPCHK(c, hipMemcpy(const_cast<float4*>(c->scene.light_rec) + 7 * e + 6, &v, sizeof v, hipMemcpyHostToDevice));
+    }
+    ++c->scene_epoch;                    // primary records hold the hit material's emission
     return PNRT_OK;
 }
 
@@ -944,6 +993,7 @@ int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int 
     HIPCHK(c, sync_all(c));
     free_env(c);
     c->scene.has_hdr = 0;
+    ++c->scene_epoch;                    // a primary miss records the env colour
     if (!rgb) return PNRT_OK;
     if (!rnd || w <= 0 || h <= 0) return set_err(c, PNRT_E_ARG, "upload_env: bad arguments");
     std::vector<float4> a((size_t)w * h), b((size_t)w * h);
@@ -968,6 +1018,7 @@ int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
     HIPCHK(c, sync_all(c));
     free_env(c);
     c->scene.has_hdr = 0;
+    ++c->scene_epoch;                    // a primary miss records the env colour
     const size_t n = (size_t)w * h;
     std::vector<float4> a(n);
     for (size_t i = 0; i < n; ++i) a[i] = make_float4(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], 0.f);
@@ -1061,6 +1112,12 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
         s.tex_w[i] = c->tex_w[i]; s.tex_h[i] = c->tex_h[i];
     }
     s.unorm8 = c->unorm8;
+    s.fault = c->fault_dev;
+    s.diag_force = 0;
+    if (WF_DIAG_BOUNDS) {                // the bounds check's own test (diagnostic builds only)
+        const char* f = getenv("PNRT_DIAG_FORCE_OOB");
+        s.diag_force = (f && atoi(f) > 0) ? 1 : 0;
+    }
     if (c->kernel == 1) {
         dim3 grid((c->width + 15) / 16, (fp.rows + 15) / 16);
         {
@@ -1068,18 +1125,20 @@ int pnrt_render(pnrt_ctx* c, uint32_t first, uint32_t nf, int band, int nsh, int
             hipLaunchKernelGGL(pt_render_kernel, grid, dim3(256), 0, c->stream, s, fp, c->accum);
         }
         HIPCHK(c, hipGetLastError());
-        return PNRT_OK;
+        return mark_stream(c);           // (every op queued on c->stream records ev_last)
     }
     return render_wavefront(c, s, fp, first, nf);
-    return set_err(c, PNRT_E_STATE, "unknown kernel variant");
 }
 
 int pnrt_reset_accum(pnrt_ctx* c) {
     if (!c) return PNRT_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    // a new accumulation: wait for the calls in flight first, so a fault of one of
+    // them (whose contribution the reset erases) is read and cleared here, not
+    // reported against the new accumulation later
+    HIPCHK(c, sync_all(c));
     (void)check_fault(c);
-    if (c->faulted) {                 // a new accumulation: wait for the calls in flight, clear the fault
-        HIPCHK(c, sync_all(c));
+    if (c->faulted) {
         for (int k = 0; k < WF_FAULT_WORDS; ++k) __atomic_store_n(c->fault_host + k, 0u, __ATOMIC_RELEASE);
         c->faulted = false;
         c->fault_msg.clear();

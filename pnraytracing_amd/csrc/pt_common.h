@@ -77,6 +77,9 @@ struct DevScene {
     const uint32_t* tex[PT_MAX_TEXTURES];   // RGBA8 texels
     int tex_w[PT_MAX_TEXTURES], tex_h[PT_MAX_TEXTURES];
     const float* unorm8;        // 256-entry c/255 table
+    int n_leaf_table;           // entries of leaf_table (>= 1)
+    uint32_t* fault;            // the context's fault words (WF_DIAG_BOUNDS builds report through them)
+    int diag_force;             // WF_DIAG_BOUNDS builds: PNRT_DIAG_FORCE_OOB (one forced out-of-range fetch)
 };
 
 struct FrameParams {

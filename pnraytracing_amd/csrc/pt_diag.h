@@ -1,21 +1,24 @@
 // pnraytracing_amd/csrc/pt_diag.h -- the ONE place the diagnostic build switches
 // live.  All default to 0, which is the product library; the others exist for
-// measurement builds (tools/build_variants.sh -> pnraytracing_amd/variants/)
-// and never ship as libpnrt.so:
+// measurement and fault-injection builds (build.py DIAG_VARIANTS,
+// tools/build_variants.sh -> pnraytracing_amd/variants/) and never ship as
+// libpnrt.so (pnrt_version() then says DIAGNOSTIC BUILD):
 //   WF_STATS        trace-kernel census: lane steps / rays per launch (tools/census.py)
 //   WF_TIMING       per-wave timestamps of the trace kernel (drain-tail analysis)
-//   WF_KO_ATTR      knockout: hit attributes without the vertex fetches   -- WRONG IMAGES
-//   WF_KO_ENV       knockout: env lookups without math (1) or memory (2)  -- WRONG IMAGES
-//   WF_DIAG_NOSTORE knockout: trace results dropped                       -- WRONG IMAGES
-//   WF_DIAG_VALU    N extra VALU instructions per traversal step (issue-bound probe)
-//   WF_KO_STATE     knockout: the path state the trace does not read (P2-P5: BRDF
-//                   value, MIS candidates, Lo, seed) neither stored by the setups nor
-//                   loaded by the shade -- register stand-ins; P0 / P1 / P7 (the
-//                   rays) and P6 (throughput, meta: control flow) kept -- WRONG IMAGES
 //   WF_DIAG_GUARD   N > 0: the trace kernel's block-queue claim gives up after N
-//                   iterations instead of 1024, so waves quit with rays unclaimed --
+//                   attempts instead of 1024, so waves quit with rays unclaimed --
 //                   WRONG IMAGES; exercises the fault report (PNRT_E_TRACE)
-// The knockouts change results, so they require -DPNRT_DIAG_BUILD as well.
+//   WF_DIAG_BOUNDS  every fetch / store index of the integrator kernels (nodes,
+//                   triangles, attributes, leaf table, stack spill area, ray and
+//                   path-state entries, light records, env footprints, albedo
+//                   texels, primary records, colours, trace results) is checked
+//                   against its array (PT_CHECK); a violation writes its site into
+//                   fault word WF_FAULT_BOUNDS (pnrt_* then return PNRT_E_TRACE) and
+//                   the index is clamped to 0, so no access leaves its array.  Same
+//                   images when nothing trips.  PNRT_DIAG_FORCE_OOB=1 in the
+//                   environment makes one gen fetch out of range (the check's test)
+// The measured-and-dropped variants and the knockouts of rounds 1-3 (DESIGN.md
+// section 8) live in git history, not here.
 #pragma once
 #ifndef WF_STATS
 #define WF_STATS 0
@@ -23,25 +26,39 @@
 #ifndef WF_TIMING
 #define WF_TIMING 0
 #endif
-#ifndef WF_KO_ATTR
-#define WF_KO_ATTR 0
-#endif
-#ifndef WF_KO_ENV
-#define WF_KO_ENV 0
-#endif
-#ifndef WF_DIAG_NOSTORE
-#define WF_DIAG_NOSTORE 0
-#endif
-#ifndef WF_DIAG_VALU
-#define WF_DIAG_VALU 0
-#endif
-#ifndef WF_KO_STATE
-#define WF_KO_STATE 0
-#endif
 #ifndef WF_DIAG_GUARD
 #define WF_DIAG_GUARD 0
 #endif
-#if (WF_KO_ATTR || WF_KO_ENV || WF_KO_STATE || WF_DIAG_NOSTORE || WF_DIAG_GUARD) && !defined(PNRT_DIAG_BUILD)
-#error "result-changing knockout switches need -DPNRT_DIAG_BUILD (measurement builds only)"
+#ifndef WF_DIAG_BOUNDS
+#define WF_DIAG_BOUNDS 0
 #endif
-#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_KO_ATTR || WF_KO_ENV || WF_KO_STATE || WF_DIAG_NOSTORE || WF_DIAG_VALU || WF_DIAG_GUARD)
+#if WF_DIAG_GUARD && !defined(PNRT_DIAG_BUILD)
+#error "result-changing diagnostic switches need -DPNRT_DIAG_BUILD (measurement builds only)"
+#endif
+#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS)
+
+// Fault words (the context's host-mapped fault area, see pt_wf.h wf_fault)
+#define WF_FAULT_GUARD 0     // a bounded wait of the block-level ray queue ran out (diagnostic builds)
+#define WF_FAULT_BLOCK 1     // a trace block loaded fewer rays than it dequeued
+#define WF_FAULT_DRAIN 2     // a trace launch ended with queue items never dequeued
+#define WF_FAULT_BOUNDS 3    // WF_DIAG_BOUNDS: an index outside its array (the word holds its PtSite)
+#define WF_FAULT_WORDS 4
+
+// PT_CHECK(fault, index, n, site): the index itself in product builds; in
+// WF_DIAG_BOUNDS builds an index outside [0, n) records `site` and reads as 0.
+#if WF_DIAG_BOUNDS
+PN_DEV long long pt_check_bound(uint32_t* fault, long long idx, long long n, int site) {
+    if ((unsigned long long)idx < (unsigned long long)n) return idx;
+    if (fault) __hip_atomic_store(fault + WF_FAULT_BOUNDS, (uint32_t)site, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return 0;
+}
+#define PT_CHECK(fault, idx, n, site) pt_check_bound((fault), (long long)(idx), (long long)(n), (site))
+#else
+#define PT_CHECK(fault, idx, n, site) (idx)
+#endif
+// check sites (the number a WF_FAULT_BOUNDS report carries; pnrt_device.hip check_fault names them)
+enum PtSite {
+    PT_SITE_NODE = 1, PT_SITE_TRI, PT_SITE_LEAF_TABLE, PT_SITE_SPILL, PT_SITE_RESULT, PT_SITE_RAY,
+    PT_SITE_HIT_ATTR, PT_SITE_LIGHT_REC, PT_SITE_ENV_QUAD, PT_SITE_TEXEL, PT_SITE_PRIMARY, PT_SITE_COLOR,
+    PT_SITE_PATH, PT_SITE_SEGMENT
+};

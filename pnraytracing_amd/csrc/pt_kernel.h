@@ -110,7 +110,7 @@ PN_DEV void decode_leaf(const DevScene& s, uint32_t ref, int& start, int& cnt) {
         asm("v_and_b32 %0, 0xffffff, %1" : "=v"(start) : "v"(ref));
         cnt = (int)((ref >> 24) & 0x7fu);
     } else if (ref & REF_TABLE) {
-        int2 e = s.leaf_table[ref & 0x3fffffffu];
+        int2 e = s.leaf_table[PT_CHECK(s.fault, ref & 0x3fffffffu, s.n_leaf_table, PT_SITE_LEAF_TABLE)];
         start = e.x; cnt = e.y;
     } else {
         start = (int)((ref >> 7) & 0x7fffffu);

@@ -48,15 +48,12 @@ struct HitFetch {
     float4 t0, t1, t2, a0, a1, a2, a3;
 };
 PN_DEV HitFetch hit_fetch(const DevScene& s, int tri) {
+    tri = (int)PT_CHECK(s.fault, tri, s.n_tris, PT_SITE_HIT_ATTR);
     HitFetch f;
     const float4* t = s.tris + 3 * (size_t)tri;
     f.t0 = t[0]; f.t1 = t[1]; f.t2 = t[2];
-    if (WF_KO_ATTR) {
-        f.a0 = f.a1 = f.a2 = f.a3 = make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-        const float4* ta = s.tri_attr + 4 * (size_t)tri;
-        f.a0 = ta[0]; f.a1 = ta[1]; f.a2 = ta[2]; f.a3 = ta[3];
-    }
+    const float4* ta = s.tri_attr + 4 * (size_t)tri;
+    f.a0 = ta[0]; f.a1 = ta[1]; f.a2 = ta[2]; f.a3 = ta[3];
     return f;
 }
 // Shading data of the accepted triangle (TriangleIntersect :320-355), recomputed

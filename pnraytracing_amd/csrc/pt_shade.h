@@ -54,22 +54,11 @@ PN_DEV int wrap_repeat(float fl, int n) {
 }
 // A bilinear lookup split into its fetch (the four texels) and its weighting,
 // so callers can put independent fetches in flight before using the result;
-// sample = taps_resolve(taps_fetch(...)) is the one-piece lookup.
+// sample = taps_resolve(taps_quad(...)) is the one-piece lookup.
 struct Taps4 {
     float4 t00, t10, t01, t11;
     float a, b;
 };
-PN_DEV Taps4 taps_clamp(const float4* img, int w, int h, float u, float v) {
-    Taps4 t;
-    float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
-    float flu = floorf(fu), flv = floorf(fv);
-    t.a = fu - flu; t.b = fv - flv;
-    int i0 = wrap_clamp(flu, w), i1 = wrap_clamp(flu + 1.0f, w);
-    int j0 = wrap_clamp(flv, h), j1 = wrap_clamp(flv + 1.0f, h);
-    t.t00 = img[(size_t)j0 * w + i0]; t.t10 = img[(size_t)j0 * w + i1];
-    t.t01 = img[(size_t)j1 * w + i0]; t.t11 = img[(size_t)j1 * w + i1];
-    return t;
-}
 PN_DEV f3 taps_resolve(const Taps4& t) {
     const float a = t.a, b = t.b;
     float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
@@ -77,18 +66,14 @@ PN_DEV f3 taps_resolve(const Taps4& t) {
                ((w00 * t.t00.y + w10 * t.t10.y) + w01 * t.t01.y) + w11 * t.t11.y,
                ((w00 * t.t00.z + w10 * t.t10.z) + w01 * t.t01.z) + w11 * t.t11.z);
 }
-PN_DEV f3 sample_clamp(const float4* img, int w, int h, float u, float v) {
-    return taps_resolve(taps_clamp(img, w, h, u, v));
-}
-// taps_clamp through the footprint records (DevScene::hdr_q / rnd_q): the same
-// four texels, bit for bit, from one 64-B record instead of two image rows.
-// Left column i0 and right column i1 = clamp(i0 + 1) select record qi = i0 + 1,
-// except at the left edge (i0 = i1 = 0: record 0, both columns 0).
-#ifndef PT_ENV_QUAD
-#define PT_ENV_QUAD 1
-#endif
-PN_DEV Taps4 taps_quad(const float4* img, const float4* quads, int w, int h, float u, float v) {
-    if (!PT_ENV_QUAD) return taps_clamp(img, w, h, u, v);
+// GL's LINEAR filter with CLAMP_TO_EDGE on a w x h image (texel (i, j) at
+// j * w + i; u * w - 0.5, floor, frac) through the footprint records
+// (DevScene::hdr_q / rnd_q): the four texels, bit for bit, from one 64-B record
+// instead of two image rows (+1.1 % C2).  Left column i0 and right column i1 =
+// clamp(i0 + 1) select record qi = i0 + 1, except at the left edge (i0 = i1 = 0:
+// record 0, both columns 0).
+PN_DEV Taps4 taps_quad(const DevScene& s, const float4* quads, float u, float v) {
+    const int w = s.hdr_w, h = s.hdr_h;
     Taps4 t;
     float fu = u * (float)w - 0.5f, fv = v * (float)h - 0.5f;
     float flu = floorf(fu), flv = floorf(fv);
@@ -96,7 +81,8 @@ PN_DEV Taps4 taps_quad(const float4* img, const float4* quads, int w, int h, flo
     int i0 = wrap_clamp(flu, w), i1 = wrap_clamp(flu + 1.0f, w);
     int j0 = wrap_clamp(flv, h), j1 = wrap_clamp(flv + 1.0f, h);
     const int qi = (i1 == i0 && i0 == 0) ? 0 : i0 + 1, qj = (j1 == j0 && j0 == 0) ? 0 : j0 + 1;
-    const float4* r = quads + (WF_KO_ENV == 2 ? 0 : 4 * ((size_t)qj * (size_t)(w + 1) + (size_t)qi));
+    const float4* r = quads + 4 * PT_CHECK(s.fault, (size_t)qj * (size_t)(w + 1) + (size_t)qi,
+                                           (size_t)(w + 1) * (size_t)(h + 1), PT_SITE_ENV_QUAD);
     t.t00 = r[0]; t.t10 = r[1]; t.t01 = r[2]; t.t11 = r[3];
     return t;
 }
@@ -123,8 +109,11 @@ PN_DEV AlbedoTaps albedo_fetch(const DevScene& s, int t, float u, float v) {
     r.a = fu - flu; r.b = fv - flv;
     int i0 = wrap_repeat(flu, w), i1 = wrap_repeat(flu + 1.0f, w);
     int j0 = wrap_repeat(flv, h), j1 = wrap_repeat(flv + 1.0f, h);
-    r.t00 = img[(size_t)j0 * w + i0]; r.t10 = img[(size_t)j0 * w + i1];
-    r.t01 = img[(size_t)j1 * w + i0]; r.t11 = img[(size_t)j1 * w + i1];
+    const size_t n = (size_t)w * h;
+    r.t00 = img[PT_CHECK(s.fault, (size_t)j0 * w + i0, n, PT_SITE_TEXEL)];
+    r.t10 = img[PT_CHECK(s.fault, (size_t)j0 * w + i1, n, PT_SITE_TEXEL)];
+    r.t01 = img[PT_CHECK(s.fault, (size_t)j1 * w + i0, n, PT_SITE_TEXEL)];
+    r.t11 = img[PT_CHECK(s.fault, (size_t)j1 * w + i1, n, PT_SITE_TEXEL)];
     return r;
 }
 PN_DEV f3 albedo_resolve(const AlbedoTaps& r) {
@@ -157,12 +146,11 @@ PN_DEV f3 sample_albedo(const DevScene& s, int t, float u, float v) {
 // GetHDRImageColor (:181-193), invAtan = (0.1591, 0.3183) as written
 PN_DEV f3 env_color(const DevScene& s, f3 v) {
     if (!s.has_hdr) return mk3(0.f, 0.f, 0.f);
-    if (WF_KO_ENV == 1) return mk3(v.x * 0.5f, 0.5f, 0.5f);
     float u = pnm_atan2(v.z, v.x), w = pnm_asin(v.y);
     u = u * 0.1591f; w = w * 0.3183f;
     u = u + 0.5f; w = w + 0.5f;
     w = 1.0f - w;
-    return taps_resolve(taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, u, w));
+    return taps_resolve(taps_quad(s, s.hdr_q, u, w));
 }
 
 // SampleHDRImage (:560-576) in two halves: env_dir turns the RandomHDR taps at
@@ -180,12 +168,12 @@ PN_DEV Taps4 env_dir(const DevScene& s, const Taps4& paramTaps, f3& L, float& pd
     float sinTheta = fmax_(1e-10f, st);
     float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
     pdf = pdf * convert;
-    return taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, param.x, param.y);
+    return taps_quad(s, s.hdr_q, param.x, param.y);
 }
 
 // SampleHDRImage (:560-576); r1, r2 drawn by the caller in order
 PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
-    f3 param = WF_KO_ENV == 1 ? mk3(r1, r2, 0.5f) : taps_resolve(taps_quad(s.rnd, s.rnd_q, s.hdr_w, s.hdr_h, r1, r2));
+    f3 param = taps_resolve(taps_quad(s, s.rnd_q, r1, r2));
     param.y = 1.0f - param.y;
     float phi = (2.0f * PT_PI) * (param.x - 0.5f);
     float theta = PT_PI * (param.y - 0.5f);
@@ -197,8 +185,7 @@ PN_DEV f3 sample_env(const DevScene& s, float r1, float r2, f3& L, float& pdf) {
     float sinTheta = fmax_(1e-10f, st);
     float convert = (float)(s.hdr_w * s.hdr_h / 2) / (((2.0f * PT_PI) * PT_PI) * sinTheta);
     pdf = pdf * convert;
-    if (WF_KO_ENV == 1) return mk3(param.x, param.y, 0.5f);
-    return taps_resolve(taps_quad(s.hdr, s.hdr_q, s.hdr_w, s.hdr_h, param.x, param.y));
+    return taps_resolve(taps_quad(s, s.hdr_q, param.x, param.y));
 }
 
 // ---- Disney BRDF (:649-849) -------------------------------------------------------

@@ -36,11 +36,7 @@
 #ifndef WF_SMALL_CALL_PATHS
 #define WF_SMALL_CALL_PATHS 5000000   // calls with fewer paths (multi-GPU shares: 2.1M at N = 8, 4.2M at N = 4 with 8-frame calls) use all WF_PIPES sets
 #endif
-#ifndef WF_SPLIT
-#define WF_SPLIT 0          // also split each frame group into two concurrent half-batches (2 streams per call)
-#endif
 #define WF_LIGHT_SCAN PT_LIGHT_SCAN
-#define WF_OVF 56
 #ifndef WF_QSHARDS
 #define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
 #endif
@@ -52,57 +48,24 @@
 #endif
 #define WF_SPA_STRIDE (WF_TRACE_BLOCK * 8u)                 // LDS bytes per stack depth
 #define WF_SPA_SHIFT (WF_TRACE_BLOCK == 512 ? 12 : WF_TRACE_BLOCK == 256 ? 11 : 10)
-#define WF_CHUNK 256u        // rays per dequeue
-#ifndef WF_SUB
-#define WF_SUB 256          // rays per dequeue (a divisor of the 256-ray segment)
-#endif
-#define WF_NSUB (256 / WF_SUB)
 #define WF_BQ_GUARD (WF_DIAG_GUARD > 0 ? (uint32_t)WF_DIAG_GUARD : (1u << 10))   // block-queue claim attempts
-#ifndef WF_CONT_FROM_STATE
-#define WF_CONT_FROM_STATE 1   // continuation rays are traced from the path state (P0, P1), not queued
-#endif
-#ifndef WF_LIGHT_FROM_STATE
-#define WF_LIGHT_FROM_STATE 1  // light shadow rays are traced from the path state (P0, P7), not queued
-#endif
-// ray kinds: 0 light shadow, 1 env shadow, 2 continuation; which have queued records,
-// and each queued kind's index among them (its npad-slot range in rayO / rayD)
-#define WF_QUEUED(k) (!((k) == 0 && WF_LIGHT_FROM_STATE) && !((k) == 2 && WF_CONT_FROM_STATE))
-#define WF_NQUEUED (WF_QUEUED(0) + WF_QUEUED(1) + WF_QUEUED(2))
-PN_DEV constexpr uint32_t wf_qidx(int k) { return (k > 0 && WF_QUEUED(0)) + (k > 1 && WF_QUEUED(1)); }
+// Ray kinds: 0 light shadow, 1 env shadow, 2 continuation.  Only env shadow rays
+// are queued as ready-to-trace records (rayO / rayD): continuation and light
+// shadow rays are traced from the path state the setup wrote (P0 with P1 / P7,
+// see wf_enqueue; queued records for them measured 2 % / 3.3 % slower).
+#define WF_QUEUED(k) ((k) == 1)
 
 // Cache policy of the streamed path-state traffic (path state, ray records,
 // frame colours): written once by a setup, read once by the trace and the next
 // shade, never by the same CU's L2 while the line could still be there -- 1 GB
 // per state set, far beyond the 4 MB L2 of an XCD, which the trace kernels of
-// the calls in flight use for the BVH.  WF_LD_POLICY = 1: non-temporal loads
-// (C2 +0.5 to +1.2 %, same box).  WF_ST_POLICY = buffer-store aux bits: 0 plain
-// (kept), 16 = sc1 (write-through, the line leaves the XCD's L2: -4 %), 2 = nt
-// (neutral).
-#ifndef WF_ST_POLICY
-#define WF_ST_POLICY 0
-#endif
-#ifndef WF_LD_POLICY
-#define WF_LD_POLICY 1
-#endif
-PN_DEV void ps_st(float4* base, size_t i, float4 v) {
-    if constexpr (WF_ST_POLICY == 0) {
-        base[i] = v;
-    } else {
-        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-        u4 d;
-        d.x = __float_as_uint(v.x); d.y = __float_as_uint(v.y); d.z = __float_as_uint(v.z); d.w = __float_as_uint(v.w);
-        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)(i * 16u), 0, WF_ST_POLICY);
-    }
-}
+// the calls in flight use for the BVH.  Loads are non-temporal (C2 +0.5 to
+// +1.2 %, same box); stores plain (write-through sc1 stores: -4 %, nt: neutral).
+PN_DEV void ps_st(float4* base, size_t i, float4 v) { base[i] = v; }
 PN_DEV float4 ps_ld(const float4* p) {
-#if WF_LD_POLICY == 0
-    return *p;
-#else
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
     return make_float4(v.x, v.y, v.z, v.w);
-#endif
 }
 
 // ray kinds a setup emitted (enqueue) ...
@@ -129,7 +92,7 @@ struct PathSet {
     float4* P4;   // LEnvironment.xyz, -    written iff the path has an env ray, read iff it is unoccluded
     float4* P5;   // Lo.xyz, bits(seed)
     float4* P6;   // throughput.xyz, bits(meta)
-    float4* P7;   // light shadow ray direction (WF_LIGHT_FROM_STATE; read by trace only)
+    float4* P7;   // light shadow ray direction (read by trace only)
     uint32_t* bcount;   // live paths of each setup block
 };
 
@@ -143,12 +106,12 @@ struct WfBufs {
     unsigned int* counter;   // ray dequeue counter (zeroed before each bounce)
     // ray queues, written by setup without atomics: segment (k, j) of kind k
     // (light | env | continuation) and setup block j = trace slots
-    // [k * npad + 256 j, +segcount[k * nseg_k + j]).  Queued kinds (WF_QUEUED:
-    // env) store ready-to-trace records there -- rayO = (origin, bits(path
-    // entry)), rayD = (direction, -), at wf_qidx(k) * npad + the slot's offset;
-    // the other kinds are read from the path state (see wf_enqueue)
-    float4* rayO;            // [WF_NQUEUED * npad]  (.w = path entry j)
-    float4* rayD;            // [WF_NQUEUED * npad]
+    // [k * npad + 256 j, +segcount[k * nseg_k + j]).  The queued kind (env)
+    // stores ready-to-trace records -- rayO = (origin, bits(path entry)), rayD =
+    // (direction, -), at the slot's offset within its npad entries; the other
+    // kinds are read from the path state (see wf_enqueue)
+    float4* rayO;            // [npad]  (.w = path entry j)
+    float4* rayD;            // [npad]
     unsigned int* segcount;  // [3 * nseg_k]
     uint32_t npad;           // n rounded up to 256
     uint32_t nseg_k;         // setup blocks = segments per kind
@@ -162,13 +125,10 @@ struct WfBufs {
 
 // Faults: a trace launch that could leave a queued ray untraced reports it
 // instead of returning a silently wrong image (ray_tracing.comp:429-494 traces
-// every ray).  One word per kind in the context's host-mapped fault area,
-// written with a system-scope vector store only when a check trips (pnrt_render,
-// pnrt_synchronize, pnrt_read_accum and pnrt_pack_rows then return PNRT_E_TRACE).
-#define WF_FAULT_GUARD 0     // a bounded wait of the block-level ray queue ran out
-#define WF_FAULT_BLOCK 1     // a trace block loaded fewer rays than it dequeued
-#define WF_FAULT_DRAIN 2     // a trace launch ended with queue items never dequeued
-#define WF_FAULT_WORDS 4
+// every ray).  One word per kind (pt_diag.h WF_FAULT_*) in the context's
+// host-mapped fault area, written with a system-scope vector store only when a
+// check trips (pnrt_render, pnrt_synchronize, pnrt_read_accum and pnrt_pack_rows
+// then return PNRT_E_TRACE).
 PN_DEV void wf_fault(const WfBufs& b, int kind) {
     __hip_atomic_store(b.fault + kind, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -179,7 +139,7 @@ PN_DEV void wf_fault(const WfBufs& b, int kind) {
 // passed all ceil((nseg - p) / WF_QSHARDS) tickets below nseg.
 PN_DEV void wf_check_drained(const WfBufs& b) {
     if (blockIdx.x == 0 && threadIdx.x < WF_QSHARDS) {
-        const uint32_t nseg = 3u * b.nseg_k * WF_NSUB, p = threadIdx.x;
+        const uint32_t nseg = 3u * b.nseg_k, p = threadIdx.x;
         const uint32_t need = nseg > p ? (nseg - p + WF_QSHARDS - 1) / WF_QSHARDS : 0u;
         if (b.counter[p * WF_QSTRIDE] < need) wf_fault(b, WF_FAULT_DRAIN);
     }
@@ -204,77 +164,44 @@ PN_DEV void wf_coords(const WfBufs& b, uint32_t s, int& x, int& lr, int& k) {
 PN_DEV uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-// Rank of this lane among the lanes of its 256-thread block with `live` set
-// (wave ballots + LDS), and the block's total; every thread must call it.
-PN_DEV uint32_t wf_block_rank(bool live, uint32_t& total) {
-    __shared__ uint32_t wc[4];
-    const uint64_t m = __ballot(live);
-    const int w = (int)(threadIdx.x >> 6);
-    if ((threadIdx.x & 63) == 0) wc[w] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t base = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t c = wc[k];
-        base += k < w ? c : 0u;
-        tot += c;
-    }
-    total = tot;
-    return base + lanes_below(m);
-}
-// The same compaction without a block barrier between the waves' loads: each
-// wave takes its range with one LDS atomic on the block's live-path counter
-// (zeroed by wf_live_init at the kernel's start), so a wave whose records have
-// arrived goes on to its next fetches instead of waiting for its block's slowest
-// wave.  Which range a wave gets depends on arrival order -- no result does: a
-// path's entry only names where its state, rays and trace results live.
-// WF_WAVE_RANK 1: the block's total is read after wf_enqueue's first barrier
-// (C2 shade -2.3 % against the block rank); 2: the same with one barrier less;
-// 3 (default): wf_enqueue without any barrier -- queued rays take their slots the
-// same way (one LDS atomic per wave, no direction-octant grouping: measured
-// neutral), and the last wave through writes the block's counts (shade another
-// -1.7 %, C2 +0.8 %, profiles/r03/s7/ab_enq_nobar_s15.txt).
-#ifndef WF_WAVE_RANK
-#define WF_WAVE_RANK 3
-#endif
+// A path's compacted entry within its block, without a block barrier between
+// the waves' loads: each wave takes its range with one LDS atomic on the block's
+// live-path counter (zeroed by wf_live_init at the kernel's start), so a wave
+// whose records have arrived goes on to its next fetches instead of waiting for
+// its block's slowest wave.  Which range a wave gets depends on arrival order --
+// no result does: a path's entry only names where its state, rays and trace
+// results live.  (Against a block-barrier rank: C2 shade -2.3 %; the barrier-free
+// wf_enqueue below another -1.7 %, C2 +0.8 %, profiles/r03/s7/ab_enq_nobar_s15.txt.)
 PN_DEV uint32_t* wf_live_ctr() {
     __shared__ uint32_t c;
     return &c;
 }
-#define WF_NBIN 8
-PN_DEV unsigned int (*wf_bins())[WF_NBIN + 1] {      // wf_enqueue's per-kind direction-bin counters
-    __shared__ unsigned int bin[3][WF_NBIN + 1];
-    return bin;
-}
-PN_DEV uint32_t* wf_enq_ctr() {     // WF_WAVE_RANK 3: queued rays per kind, waves through wf_enqueue
+PN_DEV uint32_t* wf_enq_ctr() {     // queued rays per kind, and the waves through wf_enqueue
     __shared__ uint32_t c[4];
     return c;
 }
 PN_DEV void wf_live_init() {
-    if (WF_WAVE_RANK) {
-        if (threadIdx.x == 0) *wf_live_ctr() = 0u;
-        if (WF_WAVE_RANK == 2 && threadIdx.x < 3 * (WF_NBIN + 1)) (&wf_bins()[0][0])[threadIdx.x] = 0u;
-        if (WF_WAVE_RANK >= 3 && threadIdx.x < 4) wf_enq_ctr()[threadIdx.x] = 0u;
-        __syncthreads();
-    }
+    if (threadIdx.x == 0) *wf_live_ctr() = 0u;
+    if (threadIdx.x < 4) wf_enq_ctr()[threadIdx.x] = 0u;
+    __syncthreads();
 }
-PN_DEV uint32_t wf_wave_rank(bool live) {
+PN_DEV uint32_t wf_entry_rank(bool live) {
     const uint64_t m = __ballot(live);
     uint32_t base = 0;
     if ((threadIdx.x & 63) == 0 && m != 0)
         base = __hip_atomic_fetch_add(wf_live_ctr(), (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return __builtin_amdgcn_readfirstlane(base) + lanes_below(m);
 }
-// A path's compacted entry within its block: the block-barrier rank, or the wave
-// rank (WF_WAVE_RANK; total is then filled in by wf_enqueue)
-PN_DEV uint32_t wf_entry_rank(bool live, uint32_t& total) {
-    if (WF_WAVE_RANK) { total = 0u; return wf_wave_rank(live); }
-    return wf_block_rank(live, total);
-}
 
-PN_DEV void wf_write_color(const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
+PN_DEV void wf_write_color(const WfBufs& b, const FrameParams& fp, float4* colors, int k, int lr, int x, f3 color) {
     color = mk3(clampf(color.x, 0.f, 1.f), clampf(color.y, 0.f, 1.f), clampf(color.z, 0.f, 1.f));
-    ps_st(colors, ((size_t)k * fp.rows + lr) * fp.width + x, make_float4(color.x, color.y, color.z, 0.f));
+    const size_t at = PT_CHECK(b.fault, ((size_t)k * fp.rows + lr) * fp.width + x,
+                               (size_t)b.chunk_frames * fp.rows * fp.width, PT_SITE_COLOR);
+    ps_st(colors, at, make_float4(color.x, color.y, color.z, 0.f));
+}
+// the primary record of local row lr, column x
+PN_DEV const float4* wf_primary(const WfBufs& b, const FrameParams& fp, const float4* primary, int lr, int x) {
+    return primary + 3 * PT_CHECK(b.fault, (size_t)lr * fp.width + x, (size_t)fp.rows * fp.width, PT_SITE_PRIMARY);
 }
 
 // Path state a bounce's setup starts from (in registers: the fused kernels
@@ -326,6 +253,7 @@ struct LightFetch {
     f3 li;
 };
 PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
+    entry = (int)PT_CHECK(s.fault, entry, s.n_lights + 1, PT_SITE_LIGHT_REC);
     LightFetch f;
     const float4* r = s.light_rec + 7 * (size_t)entry;
     f.va0 = r[0]; f.vb0 = r[1]; f.va1 = r[2]; f.vb1 = r[3]; f.va2 = r[4]; f.vb2 = r[5];
@@ -334,22 +262,18 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
     return f;
 }
 
-#ifndef WF_GEN_EARLY
-#define WF_GEN_EARLY 2      // gen: the env table taps fetched with the light record and the material
-#endif
-#ifndef WF_SOBOL_PAIR
-#define WF_SOBOL_PAIR 1     // both Sobol dimensions of a bounce in one pass over the set bits:
-#endif                      // bit 0 in the shade kernel's setup, bit 1 in gen's
-#ifndef WF_SHADE_EARLY
-#define WF_SHADE_EARLY 1    // shade: the light record with the material, the env taps later (registers)
-#endif
-// EARLY 1: the light record is fetched with the material; 2: the env table taps too.
-// Returns the ray kinds the bounce emits; writes the path state P0-P6 of entry
+// The light record is always fetched with the material.  ENV_EARLY: the env
+// table taps too (gen; in the shade kernel's setup they cost spills, -1.5 %).
+// SOBOL_PAIR: both Sobol dimensions of the bounce in one pass over the set bits
+// (sobol_pair: shade +1.1 %; in gen, where the bounce is the constant 0 and the
+// per-bit loop folds, it lost 3.5 %).
+// Returns the ray kinds the bounce emits; writes the path state P0-P7 of entry
 // i of the write set (slot = the path's (pixel, frame) slot); the rays go to `rays`.
-template <int EARLY, bool SOBOL_PAIR>
+template <bool ENV_EARLY, bool SOBOL_PAIR>
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t slot,
                               int bounce, int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const PathSet& w = b.wr;
+    i = (uint32_t)PT_CHECK(b.fault, i, b.npad, PT_SITE_PATH);
     const f3 P = q.P, N = q.N, V = q.V;
     const int hmat = q.mt & 0x00ffffff, htex = (int)((uint32_t)q.mt >> 24) - 1;
     uint32_t seed = q.seed;
@@ -360,10 +284,12 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     if (s.n_lights > 0) { u0 = rand01(seed); u1 = rand01(seed); }
     if (s.has_hdr) { r1 = rand01(seed); r2 = rand01(seed); }
     // light record (and env table taps) in flight with the material fetch
-    const LightFetch lf = light_fetch(s, light_entry(s, uSel));
+    int lentry = light_entry(s, uSel);
+    if (WF_DIAG_BOUNDS && s.diag_force && slot == 0) lentry = s.n_lights + 7;   // the check's own test
+    const LightFetch lf = light_fetch(s, lentry);
     Taps4 envTaps;
-    if constexpr (EARLY >= 2) {
-        if (s.has_hdr) envTaps = taps_quad(s.rnd, s.rnd_q, s.hdr_w, s.hdr_h, r1, r2);
+    if constexpr (ENV_EARLY) {
+        if (s.has_hdr) envTaps = taps_quad(s, s.rnd_q, r1, r2);
     }
     Material m = get_material(s, hmat);
     asm volatile("" ::: "memory");
@@ -400,20 +326,20 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         f3 lightBRDF = disney(bc, lightL);
         LD = divs(muls(mul(lightBRDF, lf.li), pnm_fabs(dot(N, lightL))), pl);
         rays.dL = ldir;
-        if (WF_LIGHT_FROM_STATE) ps_st(w.P7, i, make_float4(ldir.x, ldir.y, ldir.z, 0.f));
+        ps_st(w.P7, i, make_float4(ldir.x, ldir.y, ldir.z, 0.f));
         nfl |= WF_RLIGHT;
     }
     // stored as soon as final (shorter live ranges), and only when shade can use it:
     // shade takes (0, 0) for a path without a light ray, as the reference's
     // initial LDirect / lightPDF (:878-879)
-    if ((nfl & WF_RLIGHT) && !WF_KO_STATE) ps_st(w.P3, i, make_float4(LD.x, LD.y, LD.z, pl));
+    if (nfl & WF_RLIGHT) ps_st(w.P3, i, make_float4(LD.x, LD.y, LD.z, pl));
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
     if (s.has_hdr) {
         f3 enL;
         f3 enLi;
-        if constexpr (EARLY >= 2) enLi = taps_resolve(env_dir(s, envTaps, enL, pe));
+        if constexpr (ENV_EARLY) enLi = taps_resolve(env_dir(s, envTaps, enL, pe));
         else enLi = sample_env(s, r1, r2, enL, pe);
         if (dot(enL, N) > 0) {
             f3 dB = disney(bc, enL);
@@ -422,7 +348,7 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             nfl |= WF_RENV;
         }
     }
-    if ((nfl & WF_RENV) && !WF_KO_STATE) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
+    if (nfl & WF_RENV) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -481,25 +407,16 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
                           ((uint32_t)bounce << WF_META_BSHIFT);
     ps_st(w.P0, i, make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF));
     ps_st(w.P1, i, make_float4(L.x, L.y, L.z, NdotL));
-    if (!WF_KO_STATE) {
-        ps_st(w.P2, i, make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe));
-        ps_st(w.P5, i, make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed)));
-    } else {     // knockout: keep the values live (no dead-code elimination of their math)
-        if (__float_as_uint(dBRDF.x + pe + q.Lo.x + LD.x + LE.x + pl) == 0x7fc00001u + seed) w.P2[i] = make_float4(0, 0, 0, 0);
-    }
+    ps_st(w.P2, i, make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe));
+    ps_st(w.P5, i, make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed)));
     ps_st(w.P6, i, make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(meta)));
     return nfl | WF_RCONT;
 }
 
 // Compact the block's rays of each kind into its own queue segment: a ballot
-// per wave, wave offsets through LDS, no global atomics.  Each ray's traversal
-// result is independent of every other ray and of its queue position.
-#ifndef WF_SORT_OCTANT
-#define WF_SORT_OCTANT 1   // order each segment by ray-direction octant
-#endif
-PN_DEV int wf_dir_bin(const f3 d) {
-    return WF_SORT_OCTANT ? (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0) : 0;
-}
+// per wave and one LDS atomic per wave for its slots, no global atomics, no
+// barrier.  Each ray's traversal result is independent of every other ray and of
+// its queue position.
 //
 // Rays traced from the path state: every live path has a continuation ray, and a
 // light shadow ray whenever the scene has lights (the setup draws one for every
@@ -507,91 +424,35 @@ PN_DEV int wf_dir_bin(const f3 d) {
 // entries [256 j, 256 j + total) -- so the segment of such a kind IS that range
 // of the path state: origin P0.xyz (the offset origin both kinds start from),
 // direction P1.xyz (continuation) or P7.xyz (light), the same floats a ray
-// record would copy.  Only the count is stored.  (Sorting continuation rays by
-// octant measured neutral, 2 x 3 runs.)
-PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays, uint32_t total,
-                       bool lights) {
-    // Inside a segment the rays are grouped by direction bin: rays with the same
-    // signs take the same near/far choice at every node (:448), so a wave walks
-    // the tree more coherently.  Slots within a bin come from LDS atomics (order
-    // not deterministic, which no result depends on).
-    unsigned int (*bin)[WF_NBIN + 1] = wf_bins();
-    const uint32_t need[3] = {WF_RLIGHT, WF_RENV, WF_RCONT};
-    if (WF_WAVE_RANK >= 3) {
-        // no barrier: a queued kind's slots from one LDS atomic per wave (no octant
-        // grouping), and the wave that passes through here last writes the block's
-        // counts (its acquire sees every other wave's counter updates)
-        uint32_t* ec = wf_enq_ctr();
-        const int lane = threadIdx.x & 63;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (!WF_QUEUED(k)) continue;
-            const uint64_t m = __ballot((nfl & need[k]) != 0u);
-            uint32_t base = 0;
-            if (lane == 0 && m != 0)
-                base = __hip_atomic_fetch_add(ec + k, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (nfl & need[k]) {
-                const size_t slot = (size_t)wf_qidx(k) * b.npad + (size_t)blockIdx.x * 256 + base + lanes_below(m);
-                const f3 o = k == 1 ? rays.oP : rays.oOff;
-                const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
-                ps_st(b.rayO, slot, make_float4(o.x, o.y, o.z, __uint_as_float(i)));
-                ps_st(b.rayD, slot, make_float4(d.x, d.y, d.z, 0.f));
-            }
-        }
-        uint32_t done = 0;
-        if (lane == 0) done = __hip_atomic_fetch_add(ec + 3, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__builtin_amdgcn_readfirstlane(done) == blockDim.x / 64 - 1) {
-            const uint32_t tot = __hip_atomic_load(wf_live_ctr(), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (lane < 3) {
-                const uint32_t qn = __hip_atomic_load(ec + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                b.segcount[lane * b.nseg_k + blockIdx.x] = WF_QUEUED(lane) ? qn : ((lane == 2 || lights) ? tot : 0u);
-            }
-            if (lane == 0) b.wr.bcount[blockIdx.x] = tot;
-        }
-        return;
-    }
-    if (WF_WAVE_RANK < 2) {                 // (WF_WAVE_RANK 2: zeroed by wf_live_init)
-        for (int k = threadIdx.x; k < 3 * (WF_NBIN + 1); k += blockDim.x) (&bin[0][0])[k] = 0;
-        __syncthreads();
-        if (WF_WAVE_RANK) total = *wf_live_ctr();    // every wave counted its live paths before the barrier
-        if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
-    }
-    int oct[3];
-    unsigned int rank[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        if (!WF_QUEUED(k)) continue;
-        const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
-        oct[k] = wf_dir_bin(d);
-        rank[k] = (nfl & need[k]) ? atomicAdd(&bin[k][oct[k]], 1u) : 0u;
-    }
-    __syncthreads();
-    if (WF_WAVE_RANK >= 2) {
-        total = *wf_live_ctr();
-        if (threadIdx.x == 0) b.wr.bcount[blockIdx.x] = total;
-    }
-    if (threadIdx.x < 3) {
-        const int k = threadIdx.x;
-        if (WF_QUEUED(k)) {                   // exclusive prefix over the bins of a kind
-            unsigned int run = 0;
-            for (int o = 0; o < WF_NBIN; ++o) { const unsigned int c = bin[k][o]; bin[k][o] = run; run += c; }
-            bin[k][WF_NBIN] = run;
-            b.segcount[k * b.nseg_k + blockIdx.x] = run;
-        } else {
-            b.segcount[k * b.nseg_k + blockIdx.x] = (k == 2 || lights) ? total : 0u;
+// record would copy.  Only the count is stored.  The env shadow rays (drawn only
+// where the sampled direction is above the surface) are queued as records.  The
+// wave that passes through here last writes the block's counts (its acquire sees
+// every other wave's counter updates).  (Grouping a segment's rays by direction
+// octant measured neutral for both queued and state-traced kinds.)
+PN_DEV void wf_enqueue(const WfBufs& b, uint32_t i, uint32_t nfl, const BounceRays& rays, bool lights) {
+    uint32_t* ec = wf_enq_ctr();
+    const int lane = threadIdx.x & 63;
+    {   // env shadow rays: ready-to-trace records
+        const uint64_t m = __ballot((nfl & WF_RENV) != 0u);
+        uint32_t base = 0;
+        if (lane == 0 && m != 0)
+            base = __hip_atomic_fetch_add(ec + 1, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (nfl & WF_RENV) {
+            const size_t slot = PT_CHECK(b.fault, (size_t)blockIdx.x * 256 + base + lanes_below(m), b.npad, PT_SITE_RAY);
+            ps_st(b.rayO, slot, make_float4(rays.oP.x, rays.oP.y, rays.oP.z, __uint_as_float(i)));
+            ps_st(b.rayD, slot, make_float4(rays.dE.x, rays.dE.y, rays.dE.z, 0.f));
         }
     }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        if (WF_QUEUED(k) && (nfl & need[k])) {
-            const size_t slot = (size_t)wf_qidx(k) * b.npad + (size_t)blockIdx.x * 256 + bin[k][oct[k]] + rank[k];
-            const f3 o = k == 1 ? rays.oP : rays.oOff;
-            const f3 d = k == 0 ? rays.dL : (k == 1 ? rays.dE : rays.dC);
-            ps_st(b.rayO, slot, make_float4(o.x, o.y, o.z, __uint_as_float(i)));
-            ps_st(b.rayD, slot, make_float4(d.x, d.y, d.z, 0.f));
+    uint32_t done = 0;
+    if (lane == 0) done = __hip_atomic_fetch_add(ec + 3, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__builtin_amdgcn_readfirstlane(done) == blockDim.x / 64 - 1) {
+        const uint32_t tot = __hip_atomic_load(wf_live_ctr(), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane < 3) {
+            const uint32_t qn = __hip_atomic_load(ec + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            b.segcount[lane * b.nseg_k + blockIdx.x] = WF_QUEUED(lane) ? qn : ((lane == 2 || lights) ? tot : 0u);
         }
+        if (lane == 0) b.wr.bcount[blockIdx.x] = tot;
     }
 }
 
@@ -616,14 +477,14 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
         int lr, k;
         wf_coords(b, i, x, lr, k);
         if (x < fp.width && lr < fp.rows) {
-            const float4* rec = primary + 3 * ((size_t)lr * fp.width + x);
+            const float4* rec = wf_primary(b, fp, primary, lr, x);
             const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
             const int mt = __float_as_int(q0.w);
             const f3 base = mk3(q2.y, q2.z, q2.w);
             if (mt == -1) {                                   // primary miss: env colour only
-                wf_write_color(fp, colors, k, lr, x, base);
+                wf_write_color(b, fp, colors, k, lr, x, base);
             } else if (fp.max_depth == 0) {
-                wf_write_color(fp, colors, k, lr, x, add(base, mk3(0.f, 0.f, 0.f)));
+                wf_write_color(b, fp, colors, k, lr, x, add(base, mk3(0.f, 0.f, 0.f)));
             } else {
                 py = shard_row(lr, fp.band, fp.n_shards, fp.shard);
                 frame = b.first_frame + (uint32_t)k;
@@ -637,12 +498,11 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
             }
         }
     }
-    uint32_t total;
-    const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont, total);    // compacted path entry
+    const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont);    // compacted path entry
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core<WF_GEN_EARLY, (WF_SOBOL_PAIR & 2) != 0>(s, fp, b, j, i, 0, x, py, frame, q, rays);
-    wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
+    if (cont) nfl = wf_setup_core<true, false>(s, fp, b, j, i, 0, x, py, frame, q, rays);
+    wf_enqueue(b, j, nfl, rays, s.n_lights > 0);     // every lane of the wave reaches this point
 }
 
 // ---- trace: every ray of the bounce, persistent waves, LDS short stack ------------------------
@@ -657,7 +517,7 @@ PN_DEV void decode_leaf_fast(const DevScene& s, uint32_t ref, int& start, int& c
     cnt = (int)(ref & 0x7fu);
     if (TBL) {
         if ((ref & (REF_LEAF | REF_TABLE)) == (REF_LEAF | REF_TABLE) && ref != REF_NONE) {
-            const int2 e = s.leaf_table[ref & 0x3fffffffu];
+            const int2 e = s.leaf_table[PT_CHECK(s.fault, ref & 0x3fffffffu, s.n_leaf_table, PT_SITE_LEAF_TABLE)];
             start = e.x;
             cnt = e.y;
         }
@@ -694,6 +554,7 @@ PN_DEV void wf_push(uint2* lds, const WfBufs& b, uint32_t& spa, bool push, uint3
     const uint2 e = make_uint2(ref, __float_as_uint(z));
     *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + min(spa, wf_spare<STK>())) = e;
     if (push & (spa >= STK * WF_SPA_STRIDE)) {
+        (void)PT_CHECK(b.fault, (spa >> WF_SPA_SHIFT) - STK, b.ovf_stride, PT_SITE_SPILL);
         const u2 v = {e.x, e.y};
         __builtin_amdgcn_raw_buffer_store_b64(v, wf_ovf_rsrc(b, STK), (int)spa, wf_ovf_soff(b), 0);
     }
@@ -708,6 +569,7 @@ PN_DEV uint2 wf_pop(const uint2* lds, const WfBufs& b, uint32_t& spa, bool pop) 
     // LDS read into one flat load (a flat load waits for every outstanding
     // vector-memory operation, stores included)
     if (pop & (pa >= STK * WF_SPA_STRIDE)) {
+        (void)PT_CHECK(b.fault, (pa >> WF_SPA_SHIFT) - STK, b.ovf_stride, PT_SITE_SPILL);
         const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)pa, wf_ovf_soff(b), 0);
         e = make_uint2(v.x, v.y);
     }
@@ -760,15 +622,6 @@ PN_DEV bool box_fast(const RayP& r, float mnx, float mny, float mnz, float mxx, 
     return box_slabs<IDENT>(r, fx, fy, fz, nx, ny, nz, zlo);
 }
 
-#ifndef WF_BLOCKQ
-#define WF_BLOCKQ 1         // block-level ray queue shared by a block's waves (see the trace kernel)
-#endif
-#ifndef WF_BQ_PREFETCH
-#define WF_BQ_PREFETCH 0    // block queue: fetch the next segment when fewer rays than this remain (0 = off)
-#endif
-#ifndef WF_RAY_PF
-#define WF_RAY_PF 0         // ray-record prefetch distance in dequeue tickets (0 = off; see the trace kernel)
-#endif
 #ifndef WF_KIND_ORDER
 #define WF_KIND_ORDER 0x210 // sweep order of the ray kinds, one hex digit each (0 light, 1 env, 2 continuation)
 #endif
@@ -777,27 +630,6 @@ PN_DEV float4 geo_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
     const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-
-// WF_RAY_PF: the wave that dequeues a segment also pulls the ray records of the
-// segment its counter hands out WF_RAY_PF tickets later into the caches (one
-// dword per 64 B, LDS-DMA into a scratch area: no register holds it), so that
-// segment's refills read the Infinity Cache instead of HBM.  Wave-uniform.
-PN_DEV __attribute__((always_inline)) void wf_prefetch_rays(const WfBufs& b, uint32_t item, int lane) {
-    __shared__ uint32_t pf_sink[64];
-    const uint32_t sj = __builtin_amdgcn_readfirstlane(item / WF_NSUB);
-    const uint32_t qk = sj / b.nseg_k, j = sj - qk * b.nseg_k;
-    const uint32_t kind = (uint32_t)(WF_KIND_ORDER >> (4 * (2 - (int)qk))) & 0xfu;
-    const uint32_t e = j * 256u;               // the segment's 256 entries (< npad: every array holds npad)
-    const bool fromState = !WF_QUEUED(kind);
-    const float4* O = fromState ? b.wr.P0 + e : b.rayO + (size_t)wf_qidx((int)kind) * b.npad + e;
-    const float4* D = fromState ? (kind == 0 ? b.wr.P7 : b.wr.P1) + e : b.rayD + (size_t)wf_qidx((int)kind) * b.npad + e;
-    // (inline asm: the builtin's scalar-operand form failed instruction selection
-    // in this loop; an extra vector-memory op only makes the compiler's later
-    // vmcnt waits stricter, never looser)
-    const uint32_t sink = (uint32_t)(uintptr_t)pf_sink;
-    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, off\n\tglobal_load_lds_dword %1, off"
-                 :: "v"(O + lane * 4), "v"(D + lane * 4), "s"(__builtin_amdgcn_readfirstlane(sink)) : "m0", "memory");
 }
 
 // One lane's traversal state (a ray being traced).
@@ -843,6 +675,10 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     // spill area, the result store) and the IEEE division stay in branches.
     const bool isTri = wf_has_tri<TBL>(t);
     const bool isNode = t.cur != REF_NONE;     // (a lane with pending triangles has cur = REF_NONE)
+    if (WF_DIAG_BOUNDS) {                      // (the buffer loads below are range-checked by the hardware)
+        if (isNode) (void)PT_CHECK(s.fault, t.cur, s.n_nodes, PT_SITE_NODE);
+        if (isTri) (void)PT_CHECK(s.fault, TBL ? (uint32_t)t.lt : (uint32_t)t.lt & 0xffffffu, s.n_tris, PT_SITE_TRI);
+    }
     // ---- the step's single fetch: a triangle record or a node; a lane with
     // neither asks for REF_NONE * 64, beyond the buffer's range, so its loads
     // return zeros without a cache access (it used to re-read node 0: +0.6 %)
@@ -931,15 +767,14 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
                         uint32_t& p) {
-    // slot = kind * npad + position in the kind's range; kinds traced from the state
-    // the setup wrote read path entry e, queued kinds their record (see wf_enqueue)
-    const uint32_t e = slot - kind * b.npad;
+    // slot = kind * npad + position e in the kind's range; kinds traced from the
+    // state the setup wrote read path entry e, the queued kind its record (see
+    // wf_enqueue)
+    const uint32_t e = (uint32_t)PT_CHECK(b.fault, slot - kind * b.npad, b.npad, PT_SITE_RAY);
     const bool fromState = !WF_QUEUED(kind);     // wave-uniform
-    const uint32_t ri = (kind == 0 ? wf_qidx(0) : kind == 1 ? wf_qidx(1) : wf_qidx(2)) * b.npad + e;
     const float4* O = fromState ? b.wr.P0 : b.rayO;
     const float4* D = fromState ? (kind == 0 ? b.wr.P7 : b.wr.P1) : b.rayD;
-    const uint32_t at = fromState ? e : ri;
-    const float4 ro = ps_ld(O + at), rd = ps_ld(D + at);
+    const float4 ro = ps_ld(O + e), rd = ps_ld(D + e);
     p = fromState ? e : __float_as_uint(ro.w);
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
@@ -963,7 +798,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 8      // waves per SIMD (64 VGPRs: no SLP packing, one-register stack position)
 #endif
-template <int STK, bool SYNC, bool TBL>
+template <int STK, bool TBL>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[(STK + 1) * WF_TRACE_BLOCK];     // STK depths + the spare one (wf_push)
     // nodes and triangle records through one buffer resource (32-bit offsets)
@@ -972,7 +807,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     const int tl = threadIdx.x, lane = tl & 63;
     // rays are dequeued one queue segment at a time (<= 256 rays of one kind from
     // 256 neighbouring paths, kind-major); one atomic per segment
-    const uint32_t nseg = 3u * b.nseg_k * WF_NSUB;
+    const uint32_t nseg = 3u * b.nseg_k;
     uint64_t t_start = WF_TIMING ? __builtin_amdgcn_s_memrealtime() : 0, t_exh = 0;
     // WF_STATS: per ray kind, a histogram of lane steps per ray (bucket = floor(log2(steps)))
     __shared__ unsigned int hist[WF_STATS ? 3 * 16 : 1];
@@ -993,21 +828,15 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
     int busy = 0;
     // Ray accounting: when the block's last wave leaves, every ray the block took
     // off the global queue must have been loaded into a lane (a loaded ray is always
-    // traced: the loop below ends only with no lane busy).  Block queue: generations
-    // advance only once a segment is fully claimed, and claimed rays are loaded at
-    // once (a wave claims as many as it has idle lanes), so the check is that the
-    // current generation's segment is used up.  Per-wave queue: bk_cnt[0] = rays
-    // dequeued - rays loaded.  bk_cnt[1] counts the waves that have left.
-    __shared__ uint32_t bk_cnt[2];
-    if (!WF_BLOCKQ) {
-        if (threadIdx.x == 0) bk_cnt[0] = bk_cnt[1] = 0u;
-        __syncthreads();
-    }
+    // traced: the loop below ends only with no lane busy).  Generations of the block
+    // queue advance only once a segment is fully claimed, and claimed rays are
+    // loaded at once (a wave claims as many as it has idle lanes), so the check is
+    // that the current generation's segment is used up.  bk_out counts the waves
+    // that have left.
     uint64_t last_ray = 0;      // WF_TIMING builds: (iteration, kind, lane steps) of the lane's last finished ray
     uint32_t witer = 0, witer_exh = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // iters, active, tri, node, idle-pop, refill, rays, -
 
-    auto prefetch_item = [&](uint32_t item) { if (item < nseg) wf_prefetch_rays(b, item, lane); };
     // dequeue the wave's next queue item into [next, end) / ckind, or set `exhausted`
     // (wave-uniform; lane 0 issues the atomic)
     auto dequeue = [&]() {
@@ -1024,45 +853,36 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             const uint32_t item = t * WF_QSHARDS + p;
             if (item < nseg) {
                 seg = item;
-                if (WF_RAY_PF) prefetch_item((t + WF_RAY_PF) * WF_QSHARDS + p);
                 break;
             }
             ++qpart;
         }
         if (seg >= nseg) { exhausted = true; if (WF_TIMING) { t_exh = __builtin_amdgcn_s_memrealtime(); witer_exh = witer; } }
         else {
-            // one dequeue = WF_SUB rays of a segment.  Kind order of the sweep
+            // one dequeue = one 256-ray segment.  Kind order of the sweep
             // (WF_KIND_ORDER): continuation rays (closest hit, the longest
             // traversals) first, then env shadow rays, so the launch ends
-            // on the short light shadow rays
-            const uint32_t sj = seg / WF_NSUB, part = seg - sj * WF_NSUB;
-            const uint32_t qk = sj / b.nseg_k;
-            const uint32_t j = sj - qk * b.nseg_k;
+            // on the short light shadow rays (smaller dequeue grains: -2 to -7 %)
+            const uint32_t qk = seg / b.nseg_k;
+            const uint32_t j = seg - qk * b.nseg_k;
             ckind = (uint32_t)(WF_KIND_ORDER >> (4 * (2 - (int)qk))) & 0xfu;
-            const uint32_t cnt = b.segcount[ckind * b.nseg_k + j];
-            const uint32_t lo = min(part * (uint32_t)WF_SUB, cnt);
-            next = ckind * b.npad + j * 256u + lo;
-            end = ckind * b.npad + j * 256u + min(lo + (uint32_t)WF_SUB, cnt);
-            if (!WF_BLOCKQ && lane == 0) atomicAdd(&bk_cnt[0], end - next);   // ray accounting (below)
+            next = ckind * b.npad + j * 256u;
+            end = next + b.segcount[ckind * b.nseg_k + j];
         }
     };
-#if WF_BLOCKQ
-    // Block-level ray queue (WF_BLOCKQ): the block's four waves share one dequeued
-    // segment; a wave claims as many rays as it has idle lanes with an LDS atomic
-    // on bq_claim = (generation << 16 | rays claimed), the segment of generation g
-    // is bq_seg[g & 15] = {first slot, end slot, kind}; the first wave to find it used
+    // Block-level ray queue: the block's four waves share one dequeued segment; a
+    // wave claims as many rays as it has idle lanes with an LDS atomic on bq_claim
+    // = (generation << 16 | rays claimed), the segment of generation g is
+    // bq_seg[g & 15] = {first slot, end slot, kind}; the first wave to find it used
     // up (a compare-and-swap on bq_refill) dequeues the next global segment and
     // publishes it as generation g + 1, the others sleep until then.  The last
     // segment of a block is thus worked through by all its waves, not by one.
-    // WF_BQ_PREFETCH > 0: the wave whose claim leaves fewer rays than that fetches
-    // the block's next segment into bq_pf_seg (bq_pf: 0 empty, 1 being fetched,
-    // 2 ready), so the generation switch waits for no global atomic.
-    __shared__ uint32_t bq_claim, bq_refill, bq_done, bq_pf, bq_pf_done;
-    __shared__ uint32_t bq_seg[16][3], bq_pf_seg[3];
+    // (Fetching the block's next segment ahead of need measured -0.5 %.)
+    __shared__ uint32_t bq_claim, bq_refill, bq_done, bk_out;
+    __shared__ uint32_t bq_seg[16][3];
     if (threadIdx.x == 0) {
-        bq_claim = 0u; bq_refill = 0u; bq_done = 0u; bq_pf = 0u; bq_pf_done = 0u;
+        bq_claim = 0u; bq_refill = 0u; bq_done = 0u; bk_out = 0u;
         bq_seg[0][0] = bq_seg[0][1] = 0u; bq_seg[0][2] = 0u;
-        bk_cnt[0] = bk_cnt[1] = 0u;
     }
     __syncthreads();
     // the next non-empty global segment into next / end / ckind, or exhausted
@@ -1071,6 +891,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             dequeue();
         } while (!exhausted && next >= end);
     };
+    // Every wait is bounded (WF_BQ_GUARD claim attempts, 2^16 sleeps).  A wave that
+    // runs out of attempts stops claiming; the rays stay queued for the block's other
+    // waves, and a real loss (a published segment left unclaimed, items never
+    // dequeued) trips the block / drain checks (WF_FAULT_BLOCK / _DRAIN).  The block's
+    // waves are co-resident, so the waits end; diagnostic builds report the guard too.
     auto bclaim = [&](uint32_t want) {
         for (uint32_t guard = 0; guard < WF_BQ_GUARD; ++guard) {
             uint32_t c = 0;
@@ -1082,26 +907,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (old < hi - lo) {
                 next = lo + old; end = min(next + want, hi);
                 ckind = __builtin_amdgcn_readfirstlane(bq_seg[g & 15][2]);
-                if (WF_BQ_PREFETCH && old + want + WF_BQ_PREFETCH >= hi - lo) {
-                    uint32_t got = 0;
-                    if (lane == 0) {
-                        uint32_t e = 0;
-                        got = __hip_atomic_compare_exchange_strong(&bq_pf, &e, 1u, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                                   __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
-                    }
-                    if (__builtin_amdgcn_readfirstlane(got)) {   // fetch the block's next segment now
-                        const uint32_t sn = next, se = end, sk = ckind;
-                        fetch_segment();
-                        if (lane == 0) {
-                            bq_pf_seg[0] = exhausted ? 0u : next;
-                            bq_pf_seg[1] = exhausted ? 0u : end;
-                            bq_pf_seg[2] = ckind;
-                            bq_pf_done = exhausted ? 1u : 0u;
-                            __hip_atomic_store(&bq_pf, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                        next = sn; end = se; ckind = sk; exhausted = false;
-                    }
-                }
                 return;
             }
             if (__hip_atomic_load(&bq_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) { exhausted = true; return; }
@@ -1113,24 +918,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             }
             won = __builtin_amdgcn_readfirstlane(won);
             if (won) {                          // this wave publishes generation g + 1
-                uint32_t pf = 0;
-                if (WF_BQ_PREFETCH) {
-                    for (uint32_t w = 0; w < (1u << 16); ++w) {  // a prefetch in progress: wait for it
-                        pf = __hip_atomic_load(&bq_pf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (pf != 1u) break;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    pf = __builtin_amdgcn_readfirstlane(pf);
-                }
-                if (pf == 2u) {                 // the prefetched segment
-                    next = __builtin_amdgcn_readfirstlane(bq_pf_seg[0]);
-                    end = __builtin_amdgcn_readfirstlane(bq_pf_seg[1]);
-                    ckind = __builtin_amdgcn_readfirstlane(bq_pf_seg[2]);
-                    exhausted = __builtin_amdgcn_readfirstlane(bq_pf_done) != 0u;
-                    if (lane == 0) __hip_atomic_store(&bq_pf, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {
-                    fetch_segment();            // skips empty segments
-                }
+                fetch_segment();                // skips empty segments
                 if (lane == 0) {
                     const uint32_t q = (g + 1) & 15;
                     bq_seg[q][0] = exhausted ? 0u : next;
@@ -1150,10 +938,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 __builtin_amdgcn_s_sleep(2);
             }
         }
-        exhausted = true;                       // guard: never expected -- reported, never silent
-        if (lane == 0) wf_fault(b, WF_FAULT_GUARD);
+        exhausted = true;                       // guard: this wave stops claiming (see above)
+        if (PNRT_IS_DIAG_BUILD && lane == 0) wf_fault(b, WF_FAULT_GUARD);
     };
-#endif
     // one traversal step of a busy lane, the result stored when its ray is done
     auto step_lane = [&](auto ident_tag) {
         constexpr bool ID = decltype(ident_tag)::value;
@@ -1181,23 +968,13 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (WF_STATS && done) atomicAdd(&hist[(t.rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (t.rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
-                const uint32_t kind = t.rid >> 30, p = t.rid & 0x3fffffffu;
-                if (!WF_DIAG_NOSTORE) {
-                    if (kind == 2) b.hit[p] = wf_tri_index<TBL>(t.hitTri);
-                    else b.occ[2 * (size_t)p + kind] = t.hitTri != -1 ? 1 : 0;
-                }
+                const uint32_t kind = t.rid >> 30, p = (uint32_t)PT_CHECK(b.fault, t.rid & 0x3fffffffu, b.n, PT_SITE_RESULT);
+                if (kind == 2) b.hit[p] = wf_tri_index<TBL>(t.hitTri);
+                else b.occ[2 * (size_t)p + kind] = t.hitTri != -1 ? 1 : 0;
                 busy = 0;
                 t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;     // (an any-hit ray may stop mid-tree)
             }
         }
-#if WF_DIAG_VALU
-        {   // timing diagnostic: extra VALU per iteration (is the loop issue-bound?)
-            float d = __int_as_float(t.lt);
-#pragma unroll
-            for (int q = 0; q < WF_DIAG_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(d));
-            t.lt = __float_as_int(d) == 0x7fffffff ? 0 : t.lt;
-        }
-#endif
     };
 
     for (;;) {
@@ -1206,16 +983,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         const int busy0 = WF_STATS ? __popcll(__ballot(busy != 0)) : 0;
         auto refill = [&]() {
             const uint64_t idle = __ballot(busy == 0);
-            if (idle != 0 && next >= end && !exhausted) {
-#if WF_BLOCKQ
-                bclaim((uint32_t)__popcll(idle));
-#else
-                dequeue();
-#endif
-            }
+            if (idle != 0 && next >= end && !exhausted) bclaim((uint32_t)__popcll(idle));
             if (idle != 0 && next < end) {
                 const uint32_t myid = next + lanes_below(idle);
-                if (!WF_BLOCKQ && lane == 0) atomicSub(&bk_cnt[0], min((uint32_t)__popcll(idle), end - next));
                 next = min(next + (uint32_t)__popcll(idle), end);
                 if (busy == 0 && myid < end) {
                     const uint32_t kind = ckind;
@@ -1246,7 +1016,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (exhausted) break;
             continue;
         }
-        const int thr = SYNC ? 0 : (__popcll(busym) * WF_REFILL_PCT) / 100;
+        const int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
         // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------
         // (IDENT: no lane of the wave needs the triangle test's axis permutation)
         auto run = [&](auto ident_tag) {
@@ -1259,17 +1029,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         else run(std::false_type{});
     }
     if (lane == 0) {      // the block's last wave out checks the ray accounting
-        const uint32_t out = __hip_atomic_fetch_add(&bk_cnt[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t out = __hip_atomic_fetch_add(&bk_out, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (out == WF_TRACE_BLOCK / 64 - 1) {
-#if WF_BLOCKQ
             const uint32_t c = __hip_atomic_load(&bq_claim, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
             const uint32_t q = (c >> 16) & 15;
-            const bool lost = (c & 0xffffu) < bq_seg[q][1] - bq_seg[q][0] ||
-                              __hip_atomic_load(&bq_pf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2u;
-#else
-            const bool lost = __hip_atomic_load(&bk_cnt[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
-#endif
-            if (lost) wf_fault(b, WF_FAULT_BLOCK);
+            if ((c & 0xffffu) < bq_seg[q][1] - bq_seg[q][0]) wf_fault(b, WF_FAULT_BLOCK);
         }
     }
     if (WF_TIMING && lane == 0) {      // diagnostic builds: per-wave start / queue-empty / end (100 MHz clock)
@@ -1295,14 +1059,18 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         for (int k = 0; k < 8; ++k) atomicAdd(b.stats + k, st[k]);
 }
 
-// ---- primary hits through the trace kernel's step (PT_PRIM_WF) --------------------------------
-// The primary pass (pt_passes.h pt_primary_kernel) with the branch-light unified
-// step of pt_wf_trace instead of its node / leaf loops: one camera ray per lane,
-// grid-stride over 256-pixel chunks (grid <= the trace grid, so the trace's stack
-// spill area serves it), the same visit order and culling, the same record.
-#ifndef PT_PRIM_WF
-#define PT_PRIM_WF 1        // 0: the one-lane-per-pixel loop pass of pt_passes.h (C2 neutral, D2 -4 %)
-#endif
+// ---- primary hits through the trace kernel's step --------------------------------------------
+// The primary ray has no jitter (ray_tracing.comp:980), so its closest hit is
+// traced once per pixel and reused by every frame of a call -- and of later calls
+// while the camera, frame, shard and scene stay the same (pnrt_device.hip
+// PrimKey).  The branch-light unified step of pt_wf_trace: one camera ray per
+// lane, grid-stride over 256-pixel chunks (grid <= the trace grid, so the trace's
+// stack spill area serves it), the same visit order and culling.  (Against a
+// one-lane-per-pixel node / leaf loop pass: primary 0.27 -> 0.22 ms per 1080p call,
+// D2 synchronised -4 %.)
+// Record: q0 = (P.xyz, bits(mat | (tex + 1) << 24)), q1 = (N.xyz, u), q2 = (v,
+// base.xyz); mat = -1 on a miss (base = emissive of the hit material, or the env
+// colour of the primary direction).
 #ifndef PT_PRIM_WF_WAVES
 #define PT_PRIM_WF_WAVES 7
 #endif
@@ -1370,9 +1138,9 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
                           float4* colors, uint32_t i, PathIn& q, int& bounce, uint32_t& slot, int& x, int& py,
                           uint32_t& frame) {
     const PathSet& rd = b.rd;
+    i = (uint32_t)PT_CHECK(b.fault, i, b.npad, PT_SITE_PATH);
     const float4 p0 = ps_ld(rd.P0 + i), p1 = ps_ld(rd.P1 + i), p6 = ps_ld(rd.P6 + i);
-    const float4 p2 = WF_KO_STATE ? make_float4(0.5f, 0.45f, 0.4f, 0.05f) : ps_ld(rd.P2 + i);
-    const float4 p5 = WF_KO_STATE ? make_float4(0.f, 0.f, 0.f, __uint_as_float(i * 0x9E3779B1u | 1u)) : ps_ld(rd.P5 + i);
+    const float4 p2 = ps_ld(rd.P2 + i), p5 = ps_ld(rd.P5 + i);
     const int ht = b.hit[i];
     // the light / env candidates are read only where they count: an occluded
     // light ray zeroes LDirect and lightPDF (:890), an occluded or absent env ray
@@ -1385,8 +1153,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     slot = meta & WF_META_SLOT;
     const bool useL = (meta & WF_META_RL) && !(oc & 0xffu);
     const bool useE = (meta & WF_META_RE) && !(oc >> 8);
-    const float4 p3 = WF_KO_STATE ? make_float4(0.01f, 0.01f, 0.01f, 0.2f) : ps_ld(useL ? rd.P3 + i : s.zero4);
-    const float4 p4 = WF_KO_STATE ? make_float4(0.01f, 0.01f, 0.01f, 0.f) : ps_ld(useE ? rd.P4 + i : s.zero4);
+    const float4 p3 = ps_ld(useL ? rd.P3 + i : s.zero4);
+    const float4 p4 = ps_ld(useE ? rd.P4 + i : s.zero4);
     // the continuation hit's records, in flight while the MIS sum waits for P3/P4
     // (a miss reads triangle 0's, unused; so does an index a faulted trace left
     // stale -- reported as PNRT_E_TRACE, never a wild read)
@@ -1407,8 +1175,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
             f3 enLi = env_color(s, normalize(L));
             Lo = add(Lo, divs(muls(mul(mul(cw, enLi), dBRDF), NdotL), dPDF));
         }
-        const float4 q2 = primary[3 * ((size_t)lr * fp.width + x) + 2];     // the primary hit's base colour
-        wf_write_color(fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
+        const float4 q2 = wf_primary(b, fp, primary, lr, x)[2];     // the primary hit's base colour
+        wf_write_color(b, fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
         return false;
     }
     RayP r = make_ray(mk3(p0.x, p0.y, p0.z), L, 0);        // the continuation ray as traced
@@ -1418,8 +1186,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     cw = mul(cw, divs(muls(dBRDF, NdotL), dPDF));
     ++bounce;
     if (bounce >= fp.max_depth) {
-        const float4 q2 = primary[3 * ((size_t)lr * fp.width + x) + 2];
-        wf_write_color(fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
+        const float4 q2 = wf_primary(b, fp, primary, lr, x)[2];
+        wf_write_color(b, fp, colors, k, lr, x, add(mk3(q2.y, q2.z, q2.w), Lo));
         return false;
     }
     // the next bounce starts here: its setup runs on the state in registers
@@ -1454,10 +1222,9 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     uint32_t slot = 0, frame = 0;
     if (threadIdx.x < live) cont = wf_shade_path(s, fp, b, primary, colors, i, q, bounce, slot, x, py, frame);
     if (FINAL) return;                        // bounce + 1 == max_depth: cont is false for every path
-    uint32_t total;
-    const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont, total);
+    const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont);
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core<WF_SHADE_EARLY, (WF_SOBOL_PAIR & 1) != 0>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
-    wf_enqueue(b, j, nfl, rays, total, s.n_lights > 0);     // every lane of the wave reaches this point
+    if (cont) nfl = wf_setup_core<false, true>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
+    wf_enqueue(b, j, nfl, rays, s.n_lights > 0);     // every lane of the wave reaches this point
 }

@@ -58,6 +58,12 @@ class PathTracer:
                                              N.fptr(Nd), len(Nd), N.fptr(L) if len(L) else None, len(L),
                                              ctypes.c_float(p.lights_sum_area)), "pnrt_upload_scene")
 
+    def update_materials(self, first: int, records: np.ndarray):
+        """Overwrite materials first.. with (n, 18) records in place (pnrt_update_materials:
+        the material panel's glTexSubImage1D edit, ImGuiLayer.hpp:73-83)."""
+        rec = np.ascontiguousarray(records, np.float32).reshape(-1, 18)
+        self._ck(self._lib.pnrt_update_materials(self._ctx, first, len(rec), N.fptr(rec)), "pnrt_update_materials")
+
     def upload_texture(self, slot: int, pixels: np.ndarray, width: int, height: int, channels: int):
         px = np.ascontiguousarray(pixels, np.uint8).reshape(-1)
         self._ck(self._lib.pnrt_upload_texture(self._ctx, slot, N.u8ptr(px), width, height, channels),

@@ -48,6 +48,8 @@ def test_launch_count_without_kernel_events():
     assert b.launches_per_step_of(16, 4, {}, "trace") == 4.0
     assert b.launches_per_step_of(0, 4, {"trace": {"ms_per_launch": 3.0, "launches_per_step": 1.0}}, "trace") == 1.0
     assert b.launches_per_step_of(0, 4, {}, "trace") is None
+    # steps < iters_per_call: the timed region's short calls do not count at kernel_ms's call size
+    assert b.launches_per_step_of(4, 1, {"trace": {"ms_per_launch": 3.0, "launches_per_step": 1.0}}, "trace") == 1.0
 
 
 def test_bound_derived_from_counters():
@@ -56,6 +58,20 @@ def test_bound_derived_from_counters():
     assert b.derive_bound(0.25, 0.52, 0.30) == "hbm-latency"    # C5: 1 GB scene, half the L2 lookups miss
     assert b.derive_bound(0.62, 0.90, 0.30) == "hbm"
     assert b.derive_bound(None, 0.5, 0.3) is None
+    # C4: the misses are the streamed ray records, the gathers hit
+    assert b.derive_bound(0.08, 0.36, 0.3, gather_hit=0.9) == "l2-latency"
+    assert b.derive_bound(0.27, 0.9, 0.3, gather_hit=0.4) == "hbm-latency"
+    g = b.gather_hit_rate(fetch_bytes=1.0e9, streamed_bytes=1.2e9, requested_bytes=9.0e9, rays=25e6)
+    assert abs(g - (1 - 0.4e9 / 8.1e9)) < 1e-9
+
+
+def test_parity_row_sets_interleave():
+    """The CPU leg's parity row sets: every PARITY_STEP-th row from offsets 0,
+    step/2, step/4, 3 step/4, ...: a permutation of the offsets, so the sets
+    partition the frame."""
+    b = _bench()
+    o = b.parity_offsets()
+    assert o[:4] == [0, 18, 9, 27] and sorted(o) == list(range(b.PARITY_STEP))
 
 
 def test_host_cpus_reports_affinity():

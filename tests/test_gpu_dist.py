@@ -27,6 +27,30 @@ def test_two_ranks_gather_equals_one(tmp_path):
     assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
 
 
+def test_eight_gloo_ranks_gather_equals_one(tmp_path):
+    """bench.py's N = 8 plan (8-way row bands, padding of the short shares,
+    same_on_all_ranks, 8 hardware queues and four calls in flight per rank)
+    rehearsed with 8 gloo ranks on the box's one GPU: the gathered C2 image
+    equals the N = 1 image bit for bit, and each run's own parity check (the
+    CPU leg's oracle rows of its timed image) passes (VERDICT r3 "Next" 8)."""
+    args = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-pmc", "--serial-steps", "1", "--config", "C2"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    a, b = str(tmp_path / "n1.npy"), str(tmp_path / "n8.npy")
+    subprocess.run([sys.executable, "bench.py", *args, "--save-image", a], cwd=REPO, env=env, check=True,
+                   timeout=400, stdout=subprocess.DEVNULL)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", "29547", "bench.py", "--gpus", "8",
+                        "--backend", "gloo", *args, "--save-image", b], cwd=REPO, env=env, timeout=600,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    import json
+    d = json.loads(line)
+    assert d["n_gpus"] == 8 and d["parity"]["differing"] == 0 and d["config"]["parallelism"] == "row-bands8x8"
+    x, y = np.load(a), np.load(b)
+    assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
 def _single_rank_c4(path):
     from pnraytracing_amd import scenes
     from pnraytracing_amd.tracer import PathTracer

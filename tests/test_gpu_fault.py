@@ -78,3 +78,50 @@ def test_forced_guard_expiry_is_reported():
 def test_product_library_reports_no_fault():
     out = _run(None, False)
     assert "DIAGNOSTIC" not in out
+
+
+BOUNDS_CHILD = r"""
+import os, sys
+sys.path.insert(0, {repo!r})
+from pnraytracing_amd import scenes
+from pnraytracing_amd.tracer import PathTracer, PnrtError
+
+pt = PathTracer(0)
+print("library:", pt.version())
+cases = [("C1", scenes.cornell_c1()), ("C2-small", scenes.bunny_c2(320, 180)),
+         ("C3-small", scenes.marry_c3(320, 180)), ("C4-small", scenes.teapot_c4(320, 180)), ("C5-rows", scenes.synthetic_c5(480, 270, env_w=1024, env_h=512))]
+for name, cfg in cases:
+    pt.load(cfg)
+    pt.render(0, 4)
+    pt.render(4, 4, 8, 4, 1)                  # a shard as well
+    pt.synchronize()                          # raises on any out-of-range index
+    print(name, "clean")
+if os.environ.get("PNRT_DIAG_FORCE_OOB"):
+    try:
+        pt.synchronize()
+    except PnrtError as e:
+        print("forced:", e)
+        sys.exit(7)
+print("BOUNDS-CHECK-DONE")
+"""
+
+
+def test_bounds_checked_variant():
+    """variants/libpnrt_bounds.so (-DWF_DIAG_BOUNDS): every fetch / store index of
+    the integrator kernels is checked against its array (VERDICT r3 "Next" 5).
+    C1, C2, C3 (albedo textures) and C4 at reduced size and a C5-scene frame (4.19M triangles, the wide
+    stack spill area) render with no check tripping; with PNRT_DIAG_FORCE_OOB=1
+    one forced out-of-range light-record index is reported (PNRT_E_TRACE naming
+    the site) and the child exits non-zero."""
+    lib = build.variant_path("bounds")
+    assert os.path.exists(lib), "variants/libpnrt_bounds.so not built (__graft_entry__.build())"
+    env = dict(os.environ, PNRT_DEVICE_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", BOUNDS_CHILD.format(repo=REPO)], env=env, capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0 and "BOUNDS-CHECK-DONE" in r.stdout, r.stdout + r.stderr[-3000:]
+    assert "DIAGNOSTIC BUILD" in r.stdout
+    env["PNRT_DIAG_FORCE_OOB"] = "1"
+    r = subprocess.run([sys.executable, "-c", BOUNDS_CHILD.format(repo=REPO)], env=env, capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode != 0, r.stdout
+    assert "(-6)" in r.stdout + r.stderr and "light record" in r.stdout + r.stderr, r.stdout + r.stderr[-3000:]

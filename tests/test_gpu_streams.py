@@ -47,3 +47,28 @@ def test_switch_away_from_destroyed_stream():
         got = pt.read_accum()
     bad = np.argwhere(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=-1))
     assert len(bad) == 0, f"{len(bad)} pixels differ"
+
+
+def test_v1_kernel_then_stream_switch():
+    """The v1 kernel accumulates on the context's stream directly; a stream switch
+    right after it (no synchronisation) must order the next frames after it
+    (every op queued on the stream records the context's last event)."""
+    from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_ZCULL
+    hip = _hip()
+    cfg = S.cornell_c1(96, 80)
+    ref, _ = pyoracle.Oracle(cfg).render(0, 6)
+    with PathTracer(0) as pt:
+        pt.load(cfg)
+        pt.set_options(TRAVERSE_ZCULL | KERNEL_V1)
+        s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s1)) == 0 and hip.hipStreamCreate(ctypes.byref(s2)) == 0
+        pt.set_stream(s1.value)
+        pt.render(0, 3)                     # v1: frames 0-2 blended in-kernel on s1
+        pt.set_stream(s2.value)             # no synchronisation in between
+        pt.render(3, 3)
+        pt.set_stream(None)
+        got = pt.read_accum()
+        assert hip.hipStreamSynchronize(s1) == 0 and hip.hipStreamSynchronize(s2) == 0
+        assert hip.hipStreamDestroy(s1) == 0 and hip.hipStreamDestroy(s2) == 0
+    bad = np.argwhere(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=-1))
+    assert len(bad) == 0, f"{len(bad)} pixels differ"
