@@ -17,10 +17,13 @@ scaling: the frame is fixed, its rows are split).
 
 Prints ONE JSON line (rank 0).  Roofline of the dominant kernel (pt_wf_trace),
 every figure measured by this run:
-  traffic   fabric bytes per trace launch, 2 x FETCH_SIZE + WRITE_SIZE from two
-            rocprofv3 --pmc passes that this script runs as child processes
-            BEFORE it touches the GPU (N = 1; MI355X_MICROARCH.md: gfx950
-            FETCH_SIZE counts half the bytes);
+  traffic   fabric bytes per trace launch from two rocprofv3 --pmc passes that
+            this script runs as child processes BEFORE it touches the GPU
+            (N = 1): FETCH_SIZE (the node / triangle gathers, tallied exactly) +
+            the streamed ray records / 2 (tallied at half; ray count from the
+            census of these sources) + WRITE_SIZE -- calibrated on known bytes,
+            profiles/r03/fetch_calibration.json; traffic_bounds = [1x, 2x]
+            FETCH_SIZE + WRITE_SIZE;
   kernel_ms the trace launch's EXCLUSIVE duration: HIP events around every
             trace launch during extra steps rendered with PNRT_SERIAL (one call
             in flight, full-occupancy grid), after the timed region;
@@ -30,6 +33,11 @@ WF_STATS build, profiles/census.json, used only when its source hash matches
 the loaded library) is reported beside it against the L2 bandwidth, and the
 SURVEY 8d reference-literal byte count as reference_bytes (never divided by a
 peak).  The timed steps themselves run the default pipelined renderer.
+
+After the timed region the CPU leg (rank 0) has the oracle render row sets of
+the timed image itself -- every 36th row over all its frames -- and reports
+"parity" (pixels differing, bit for bit; the run exits non-zero on any) and,
+at N = 1, the oracle's rate as cpu_baseline.
 """
 from __future__ import annotations
 

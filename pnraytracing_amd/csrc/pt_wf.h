@@ -764,6 +764,102 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
     return done;
 }
 
+// ---- wave-cooperative finish of a wave's last any-hit ray (WF_COOP_TAIL) ----------------------
+// Once the ray queue is exhausted, the end of a trace launch is set by its
+// slowest rays: a wave holding one last ray steps it alone, one dependent fetch
+// per lane step (about 1 us each), while its other 63 lanes idle -- the drain
+// tail that dominates a lone frame's trace launch (queues
+// dry after 15-37 us of a 185-us launch at 512x512).  Those last rays are mostly
+// shadow rays (the sweep ends on them), and an any-hit ray's result does not
+// depend on the visit order: occlusion is the OR over every reachable triangle
+// (every ancestor box passes the reference's slab test, :464-494) of the
+// watertight test at the ray's FIXED tMax.  So the wave's 64 lanes finish it
+// together: the ray's remaining work -- its LDS / spill stack entries, its node
+// to visit and its pending triangle range -- becomes a frontier in the wave's
+// LDS stack slots (free: every other lane is idle), and each iteration up to 64
+// lanes take one entry each: a node tests both child boxes with the same box
+// test and z-slab cull as wf_step and adds the children that pass; a leaf range
+// tests its first triangle with the same triangle test and adds the rest.  The
+// ray is occluded iff some lane accepts a triangle -- the same boolean, in
+// about tree-depth iterations instead of one per visited box.
+// Frontier capacity: (STK + 1) x 64 entries.  Up to 64 entries per iteration
+// while the frontier holds at most CAP - 128, else one (depth-first: +1 per
+// descent, at most the tree depth < 63 before a leaf), so it never overflows.
+#ifndef WF_COOP_TAIL
+#define WF_COOP_TAIL 1
+#endif
+template <int STK>
+PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo, uint2* lds, const RayP& r,
+                           float tMax, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t CAP = (STK + 1) * 64u;
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    auto slot = [&](uint32_t e) -> uint32_t {      // LDS byte address of frontier entry e
+        return (e >> 6) * WF_SPA_STRIDE + 8u * (wbase + (e & 63u));
+    };
+    const float tmc = tMax * 1.000001f;
+    const float zc = tmc <= 1e-20f ? 1e-20f : tmc;      // wf_step's cull bound (tMax is fixed)
+    const bool cull = r.cull_ok();
+    // the owner's stack: depth d < sp at spa = d * stride + 8 * otl (LDS below STK, spill area above)
+    const uint32_t sp = spa >> WF_SPA_SHIFT;
+    uint2 e = make_uint2(REF_NONE, 0u);
+    if (lane < sp) {
+        const uint32_t a = lane * WF_SPA_STRIDE + 8u * otl;
+        if (lane < (uint32_t)STK) {
+            e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
+        } else {
+            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
+            e = make_uint2(v.x, v.y);
+        }
+    }
+    // + the node it would visit next and its pending triangle range (leaf word)
+    if (lane == sp) e = make_uint2(cur, 0u);
+    if (lane == sp + 1) e = make_uint2(lt, 0u);
+    const bool valid = (lane < sp) | ((lane == sp) & (cur != REF_NONE)) |
+                       ((lane == sp + 1) & ((uint32_t)lt >= (REF_LEAF | (1u << 24))));
+    uint64_t m = __ballot(valid);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // every read of the owner's slots before the writes
+    if (valid) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(lanes_below(m))) = e;
+    uint32_t size = (uint32_t)__popcll(m);
+    bool hit = false;
+    while (size > 0) {
+        const uint32_t k = size > CAP - 128u ? 1u : min(size, 64u);
+        const bool mine = lane < k;
+        uint2 f = make_uint2(REF_NONE, 0u);
+        if (mine) f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + slot(size - 1u - lane));
+        size -= k;
+        // an entry's z: a pushed far child's z-slab lower end, culled as wf_pop culls it
+        const bool take = mine & (f.x != REF_NONE) & !(cull & (__uint_as_float(f.y) > zc));
+        const bool isTri = take & (f.x >= (REF_LEAF | (1u << 24)));
+        const bool isNode = take & ((f.x & REF_LEAF) == 0u);
+        const uint32_t offT = s.geo_tri_off + __umul24(f.x, 48u), offN = isNode ? f.x * 64u : REF_NONE * 64u;
+        const uint32_t off = isTri ? offT : offN;
+        const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
+                     q3 = geo_load(geo, offN + 48u);
+        float e0, e1, e2, det, ts;
+        const bool acc = tri_test<false>(r, q0, q1, q2, tMax, e0, e1, e2, det, ts) & isTri;
+        float zloL, zloR;
+        bool hL = box_fast<false>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+        bool hR = box_fast<false>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
+        hL = hL & !(cull & (zloL > zc)) & isNode;
+        hR = hR & !(cull & (zloR > zc)) & isNode;
+        // children to add: a node's passing children (a leaf child only if it holds
+        // triangles), a leaf range's remaining triangles
+        const uint32_t rest = f.x + (1u - (1u << 24));           // first + 1, count - 1
+        const bool cA = isTri ? (rest >= (REF_LEAF | (1u << 24))) : (hL & (__float_as_uint(q3.x) != REF_LEAF));
+        const bool cB = hR & (__float_as_uint(q3.y) != REF_LEAF);
+        const uint2 eA = isTri ? make_uint2(rest, 0u) : make_uint2(__float_as_uint(q3.x), __float_as_uint(zloL));
+        const uint2 eB = make_uint2(__float_as_uint(q3.y), __float_as_uint(zloR));
+        if (__ballot(acc) != 0) { hit = true; break; }
+        const uint64_t bA = __ballot(cA), bB = __ballot(cB);
+        const uint32_t base = size + lanes_below(bA) + lanes_below(bB);
+        if (cA) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(base)) = eA;
+        if (cB) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(base + (cA ? 1u : 0u))) = eB;
+        size += (uint32_t)(__popcll(bA) + __popcll(bB));
+    }
+    return hit;
+}
+
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
                         uint32_t& p) {
@@ -1016,7 +1112,36 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (exhausted) break;
             continue;
         }
-        const int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
+        int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
+        if (WF_COOP_TAIL && !TBL && !WF_STATS && exhausted) {
+            // the drain: a wave down to one any-hit ray finishes it with all its lanes
+            if (__popcll(busym) == 1) {
+                const int o = __ffsll((long long)busym) - 1;
+                const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
+                const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
+                if (orid < (2u << 30) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u) {
+                    auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
+                    RayP r;
+                    r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
+                    r.d = mk3(rdf(t.r.d.x), rdf(t.r.d.y), rdf(t.r.d.z));
+                    r.inv = mk3(rdf(t.r.inv.x), rdf(t.r.inv.y), rdf(t.r.inv.z));
+                    r.perm = __builtin_amdgcn_readlane(t.r.perm, o);
+                    const bool occl = wf_coop_anyhit<STK>(
+                        s, b, geo, lds, r, rdf(t.tMax), (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o),
+                        (uint32_t)__builtin_amdgcn_readlane(t.lt, o), ospa, (ospa & (WF_SPA_STRIDE - 1u)) >> 3);
+                    if (busy != 0) {
+                        const uint32_t p = (uint32_t)PT_CHECK(b.fault, t.rid & 0x3fffffffu, b.n, PT_SITE_RESULT);
+                        b.occ[2 * (size_t)p + (t.rid >> 30)] = occl ? 1 : 0;
+                        busy = 0;
+                        t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;
+                    }
+                    continue;
+                }
+                thr = 0;                 // a closest-hit ray: step it to the end
+            } else {
+                thr = max(thr, 1);       // come back here when one ray is left
+            }
+        }
         // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------
         // (IDENT: no lane of the wave needs the triangle test's axis permutation)
         auto run = [&](auto ident_tag) {

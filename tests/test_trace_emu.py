@@ -15,4 +15,7 @@ def test_packed_and_wide_ranges_agree():
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "trace_emu.py"), "150"], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "mismatches 0" in r.stdout
+    assert "rays 150 mismatches 0" in r.stdout
+    # the wave-cooperative finish of any-hit rays (pt_wf.h wf_coop_anyhit) gives the
+    # sequential traversal's occlusion from any hand-over point
+    assert "coop rays" in r.stdout and "coop rays 0 " not in r.stdout and " mismatches 0 iterations" in r.stdout

@@ -8,6 +8,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of bench.py --serial and of the default command
 #   census   trace census of these sources -> profiles/census.json (needs the stats variant)
 #   record   profiles/pmc.json from this session's N = 1 bench lines
+#   tail     WF_TIMING drain census of the lone-frame (D2) trace launches
 #   fuzz     the widened fuzz campaign (SEEDS=40000 random scenes x 3 kernel modes vs the oracle)
 # Output under gpurun_out/$TAG.  Every GPU step has its own time limit; the first failing
 # step ends the session (no retries).
@@ -45,6 +46,12 @@ for s in ${STEPS:-smoke tests bench}; do
     record)    # profiles/pmc.json from the N = 1 bench lines of this session (read by N > 1 lines)
       step record timeout -k 10 60 python tools/record_pmc.py $O/bench_C*.json
       cp profiles/pmc.json $O/pmc.json ;;
+    tail)      # WF_TIMING drain census of the lone-frame trace launches (needs variants/libpnrt_timing.so)
+      for c in ${DCONFIGS:-D2}; do
+        step tail-$c env PNRT_DEVICE_LIB=pnraytracing_amd/variants/libpnrt_timing.so timeout -k 10 200 python bench.py \
+          --config $c --sync-per-frame --steps 8 --warmup 4 --no-parity --no-pmc --serial-steps 0 > $O/tail_$c.json \
+          2> $O/tail_$c.err
+      done ;;
     fuzz)
       step fuzz env PNRT_FUZZ_SEEDS=${SEEDS:-40000} timeout -k 10 1100 python -u -m pytest tests/test_gpu_fuzz.py -x -q \
         --timeout 300 --timeout-method thread > $O/fuzz.log 2>&1

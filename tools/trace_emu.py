@@ -65,7 +65,7 @@ def box_hit(o, inv, b):
     t1 = (b[:3] - o) * inv; t2 = (b[3:] - o) * inv
     return np.max(np.minimum(t1, t2)) <= np.min(np.maximum(t1, t2))
 
-def trace(o, d, any_hit, packed):
+def trace(o, d, any_hit, packed, stop_after=None):
     inv = 1.0 / d
     tmax = 1e30
     root = childref(0, packed) if fint(N[0, 7]) == -1 else 0
@@ -77,6 +77,8 @@ def trace(o, d, any_hit, packed):
         else: cur = root
     stack, steps, trace_states = [], 0, []
     while True:
+        if stop_after is not None and steps == stop_after:      # hand the state over (packed only)
+            return None, steps, (cur, lt, list(stack))
         steps += 1
         assert steps < 100000, "runaway"
         assert len(stack) < 64, "stack overflow"
@@ -119,6 +121,39 @@ def trace(o, d, any_hit, packed):
             idx = -1 if hit == -1 else ((hit & 0xffffff) if packed else hit)
             return idx, steps, trace_states
 
+def coop(o, d, state, stk=8):
+    """pt_wf.h wf_coop_anyhit: the wave's 64 lanes finish an any-hit ray from its
+    state (node to visit, pending leaf word, stack): frontier entries taken 64 at a
+    time from the top (one at a time above CAP - 128), a node adds the children
+    whose boxes pass, a leaf word tests its first triangle and adds the rest.
+    Returns (occluded, iterations, max frontier size)."""
+    inv = 1.0 / d
+    cur, lt, stack = state
+    cap = (stk + 1) * 64
+    fr = list(stack) + ([cur] if cur != NONE else []) + ([lt] if lt >= (LEAF | (1 << 24)) else [])
+    it, peak = 0, len(fr)
+    while fr:
+        it += 1
+        k = 1 if len(fr) > cap - 128 else min(len(fr), 64)
+        take, fr = fr[len(fr) - k:], fr[:len(fr) - k]
+        new = []
+        for f in reversed(take):                 # lane i takes entry size - 1 - i
+            if f >= (LEAF | (1 << 24)):
+                if tri_hit(o, d, f & 0xffffff, 1e30) is not None:
+                    return True, it, peak
+                rest = (f + (1 - (1 << 24))) & 0xffffffff
+                if rest >= (LEAF | (1 << 24)):
+                    new.append(rest)
+            elif not (f & LEAF):
+                bl, br, rl, rr, ax = node_rec(f, True)
+                if box_hit(o, inv, bl) and rl != LEAF: new.append(rl)
+                if box_hit(o, inv, br) and rr != LEAF: new.append(rr)
+        fr += new
+        peak = max(peak, len(fr))
+        assert len(fr) <= cap, "frontier overflow"
+    return False, it, peak
+
+
 rng = np.random.default_rng(1)
 lo, hi = N[0, :3].astype(np.float64), N[0, 3:6].astype(np.float64)
 mism = 0
@@ -133,4 +168,22 @@ for r in range(NR):
         mism += 1
         if mism < 5: print("mismatch", r, a[:2], b[:2])
 print(f"rays {NR} mismatches {mism}")
-sys.exit(1 if mism else 0)
+# the cooperative finish of any-hit rays: hand over after a random number of
+# sequential steps, finish with the frontier model; the boolean must agree
+cm, its, seq, peak = 0, [], [], 0
+for r in range(NR):
+    o = lo + (hi - lo) * rng.uniform(0, 1, 3)
+    d = rng.normal(size=3); d /= np.linalg.norm(d)
+    full = trace(o, d, True, True)
+    stop = int(rng.integers(0, max(1, full[1])))
+    st = trace(o, d, True, True, stop_after=stop)
+    if st[0] is not None:                        # finished before the hand-over
+        continue
+    occ, n, pk = coop(o, d, st[2])
+    its.append(n); seq.append(full[1] - stop); peak = max(peak, pk)
+    if occ != (full[0] != -1):
+        cm += 1
+        if cm < 5: print("coop mismatch", r, occ, full[:2], stop)
+print(f"coop rays {len(its)} mismatches {cm} iterations mean {np.mean(its):.1f} vs sequential steps "
+      f"{np.mean(seq):.1f}, max frontier {peak}")
+sys.exit(1 if (mism or cm) else 0)
