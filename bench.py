@@ -571,6 +571,7 @@ def main():
 
     samples = W * H * spp * args.steps
     value = samples / elapsed / 1e6
+    parity = None
     if rank == 0:
         # one-shot setup, reported beside the step rate: host scene build
         # (ModelOutput + BuildBVH + packing), the BuildBVH part alone on the host and on
@@ -585,7 +586,7 @@ def main():
             setup["bvh_build_gpu_s"] = round(time.perf_counter() - t, 4)
             setup["bvh_gpu_identical"] = bool(np.array_equal(nodes.view(np.uint32), cfg.packed.nodes.view(np.uint32)))
 
-        cpu = counts = parity = None
+        cpu = counts = None
         if not args.no_parity:
             # the CPU leg (rank 0): oracle rows of the timed image -- its parity, and at
             # N = 1 the CPU baseline; N > 1 checks one row set (the gathered image)
