@@ -644,12 +644,28 @@ struct TravState {
     float tMax;
     int hitTri, lt, lc;       // accepted triangle; pending triangle range [lt, lt + lc)
     uint32_t spa, cur;        // stack position (see wf_push); node to visit next
-    uint32_t rid;             // kind << 30 | path: kinds 0 / 1 (shadow rays) are any-hit, kind 2 closest-hit
+    uint32_t rid;             // kind << 30 | flags | path: kinds 0 / 1 (shadow rays) are any-hit, kind 2 closest-hit
     uint32_t nst;             // WF_STATS builds: lane steps of this ray
 };
 
 template <bool TBL>
 PN_DEV bool wf_has_tri(const TravState& t) { return TBL ? t.lc > 0 : (uint32_t)t.lt >= (REF_LEAF | (1u << 24)); }
+#define WF_RID_P 0x03ffffffu          // TravState::rid: kind << 30 | flags | path entry (< 2^26)
+#define WF_RID_NOCOOP (1u << 29)      // the cooperative finish gave this ray back (traced alone to the end)
+// A ray (t.r set) starts: the root box test (:433), tMax, no hit, empty stack.
+template <bool TBL>
+PN_DEV void wf_ray_start(const DevScene& s, TravState& t, float tmax) {
+    float zlo;
+    uint32_t root = REF_NONE;
+    int nlt = 0, nlc = 0;
+    if (box_fast(t.r, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1], s.root_max[2], zlo)) {
+        root = s.root_ref;
+        if (root & REF_LEAF) { if (TBL) decode_leaf(s, root, nlt, nlc); else nlt = (int)root; root = REF_NONE; }
+    }
+    t.tMax = tmax;
+    t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
+    t.nst = 0;
+}
 // The triangle index of an accepted-hit word.  The mask goes through an opaque
 // v_and: with a plain `h & 0xffffff` feeding a 64-bit address (hit_fetch) this
 // compiler (ROCm 7.2 clang, gfx950) emitted v_mad_u64_u32 on the UNMASKED word
@@ -786,7 +802,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // while the frontier holds at most CAP - 128, else one (depth-first: +1 per
 // descent, at most the tree depth < 63 before a leaf), so it never overflows.
 #ifndef WF_COOP_TAIL
-#define WF_COOP_TAIL 1
+#define WF_COOP_TAIL 1      // 0 off, 1 any-hit rays, 2 any-hit and closest-hit rays (wf_coop_closest)
 #endif
 template <int STK>
 PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo, uint2* lds, const RayP& r,
@@ -856,6 +872,163 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
         if (cA) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(base)) = eA;
         if (cB) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(base + (cA ? 1u : 0u))) = eB;
         size += (uint32_t)(__popcll(bA) + __popcll(bB));
+    }
+    return hit;
+}
+
+// The same for a closest-hit ray, whose result is the LAST triangle the
+// reference's depth-first traversal (near child first, a leaf's triangles in
+// order, :429-461) accepts against a shrinking tMax -- an order-dependent fold,
+// exact only in that order.  Two phases:
+// 1. The frontier is walked in any order as above, each entry carrying its
+//    place in the reference's order as a 64-bit key: the rank of the hand-over
+//    entry (pending range 0, node 1, stack top 2, ... bottom), then one bit per
+//    level below it (near child 0, far child 1) ended by a sentinel bit, and the
+//    triangle's place in its leaf in the low 8 bits -- the keys of a subtree lie
+//    between its entry's key and the next one's.  Boxes are culled, and
+//    triangles accepted, against the relaxed bound E (1 + 1e-4), where E is the
+//    least hit distance found so far (from the ray's tMax at the hand-over);
+//    each accepted triangle is a candidate (key, index).
+// 2. The candidates are folded in key order from the hand-over (tMax, hit) with
+//    the exact test and tMax = ts * (1 / det): the reference's result.
+// Why the candidates suffice: let B be the least distance among the triangles
+// the exact test accepts.  Every triangle within B (1 + 5e-5) of it is a
+// candidate (E >= B, and the 1e-4 margin dwarfs the test's rounding); once the
+// reference accepts one of those, tMax <= B (1 + 5e-5) and it accepts no
+// triangle beyond B (1 + 1e-4) again, nor did anything it accepted before change
+// which of them it accepts first (all lie beyond that with margin) -- so both
+// folds accept the same triangles from there on and end on the same one.
+// Fallback: a key deeper than 47 levels below the hand-over, or a frontier plus
+// candidates beyond the capacity, returns -2 and the ray is traced again from
+// its start by its own lane (WF_RID_NOCOOP; rare, exact either way).
+template <int STK>
+PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, uint2* lds, const WfBufs& b, const RayP& r,
+                           float tMax0, int hit0, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    constexpr uint32_t CAP = (STK + 1) * 32u;           // 16-B entries: (ref, z) + key
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    auto at = [&](uint32_t i) -> char* {                 // the wave's i-th 8-B LDS slot
+        return reinterpret_cast<char*>(lds) + (i >> 6) * WF_SPA_STRIDE + 8u * (wbase + (i & 63u));
+    };
+    auto put = [&](uint32_t e, uint2 v, uint64_t key) {
+        *reinterpret_cast<uint2*>(at(2u * e)) = v;
+        *reinterpret_cast<uint2*>(at(2u * e + 1u)) = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+    };
+    const bool cull = r.cull_ok();
+    const uint64_t TOP = 1ull << 55;
+    const uint32_t sp = spa >> WF_SPA_SHIFT;
+    uint2 e = make_uint2(REF_NONE, 0u);
+    uint64_t key = 0;
+    if (lane < sp) {
+        const uint32_t a = lane * WF_SPA_STRIDE + 8u * otl;
+        if (lane < (uint32_t)STK) {
+            e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
+        } else {
+            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
+            e = make_uint2(v.x, v.y);
+        }
+        key = ((uint64_t)(2u + (sp - 1u - lane)) << 56) | TOP;
+    }
+    if (lane == sp) { e = make_uint2(cur, 0u); key = (1ull << 56) | TOP; }
+    if (lane == sp + 1) { e = make_uint2(lt, 0u); key = TOP; }
+    const bool valid = (lane < sp) | ((lane == sp) & (cur != REF_NONE)) |
+                       ((lane == sp + 1) & (lt >= (REF_LEAF | (1u << 24))));
+    const uint64_t m0 = __ballot(valid);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the owner's slots are read before any write
+    if (valid) put(lanes_below(m0), e, key);
+    uint32_t size = (uint32_t)__popcll(m0), ncand = 0;
+    float E = tMax0;
+    bool fail = false;
+    while (size > 0) {
+        const uint32_t k = size + ncand > CAP - 128u ? 1u : min(size, 64u);
+        const bool mine = lane < k;
+        uint2 f = make_uint2(REF_NONE, 0u);
+        uint64_t fk = 0;
+        if (mine) {
+            f = *reinterpret_cast<const uint2*>(at(2u * (size - 1u - lane)));
+            const uint2 kk = *reinterpret_cast<const uint2*>(at(2u * (size - 1u - lane) + 1u));
+            fk = ((uint64_t)kk.y << 32) | kk.x;
+        }
+        size -= k;
+        const float er = E * 1.0001f;                      // the relaxed bound
+        const float tmc = er * 1.000001f;
+        const float zc = tmc <= 1e-20f ? 1e-20f : tmc;
+        const bool take = mine & (f.x != REF_NONE) & !(cull & (__uint_as_float(f.y) > zc));
+        const bool isTri = take & (f.x >= (REF_LEAF | (1u << 24)));
+        const bool isNode = take & ((f.x & REF_LEAF) == 0u);
+        const uint32_t offT = s.geo_tri_off + __umul24(f.x, 48u), offN = isNode ? f.x * 64u : REF_NONE * 64u;
+        const uint32_t off = isTri ? offT : offN;
+        const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
+                     q3 = geo_load(geo, offN + 48u);
+        float e0, e1, e2, det, ts;
+        const bool acc = tri_test<false>(r, q0, q1, q2, er, e0, e1, e2, det, ts) & isTri;
+        const float th = acc ? ts * (1.0f / det) : er;
+        // E = the least distance found (a non-finite one ends the cooperation)
+        fail |= __ballot(acc & !(pnm_fabs(th) < 3.0e38f)) != 0;
+        float tmin = th;
+        for (int o = 32; o > 0; o >>= 1) tmin = fminf(tmin, __shfl_xor(tmin, o));
+        E = fminf(E, tmin);
+        float zloL, zloR;
+        bool hL = box_fast<false>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+        bool hR = box_fast<false>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
+        hL = hL & !(cull & (zloL > zc)) & isNode;
+        hR = hR & !(cull & (zloR > zc)) & isNode;
+        // children and their keys: near child (:448) = key - sent + sent / 2, far = key + sent / 2
+        const uint64_t pk = fk & ~0xffull;
+        const uint64_t sent = pk & (0ull - pk);
+        fail |= __ballot(isNode & (sent <= 0x100ull)) != 0;
+        const bool rightFirst = ((uint32_t)r.perm & __float_as_uint(q3.z)) != 0u;
+        const uint64_t kNear = fk - sent + (sent >> 1), kFar = fk + (sent >> 1);
+        const uint32_t rest = f.x + (1u - (1u << 24));           // first + 1, count - 1
+        const bool cA = isTri ? (rest >= (REF_LEAF | (1u << 24))) : (hL & (__float_as_uint(q3.x) != REF_LEAF));
+        const bool cB = hR & (__float_as_uint(q3.y) != REF_LEAF);
+        const uint2 eA = isTri ? make_uint2(rest, 0u) : make_uint2(__float_as_uint(q3.x), __float_as_uint(zloL));
+        const uint2 eB = make_uint2(__float_as_uint(q3.y), __float_as_uint(zloR));
+        const uint64_t kA = isTri ? fk + 1u : (rightFirst ? kFar : kNear), kB = rightFirst ? kNear : kFar;
+        const uint64_t bA = __ballot(cA), bB = __ballot(cB), bC = __ballot(acc);
+        const uint32_t nnew = (uint32_t)(__popcll(bA) + __popcll(bB)), nc = (uint32_t)__popcll(bC);
+        fail |= size + nnew + ncand + nc > CAP;
+        if (fail) break;
+        const uint32_t base = size + lanes_below(bA) + lanes_below(bB);
+        if (cA) put(base, eA, kA);
+        if (cB) put(base + (cA ? 1u : 0u), eB, kB);
+        // candidates from the top of the area down: (key, triangle index)
+        if (acc) put(CAP - 1u - ncand - lanes_below(bC), make_uint2(f.x & 0xffffffu, 0u), fk);
+        size += nnew;
+        ncand += nc;
+    }
+    if (fail || ncand > 64u) return -2;
+    // phase 2: the exact fold over the candidates in key (= the reference's) order
+    const bool own = lane < ncand;
+    uint32_t tri = 0;
+    uint64_t ck = ~0ull;
+    if (own) {
+        const uint2 v = *reinterpret_cast<const uint2*>(at(2u * (CAP - 1u - lane)));
+        const uint2 kk = *reinterpret_cast<const uint2*>(at(2u * (CAP - 1u - lane) + 1u));
+        tri = v.x;
+        ck = ((uint64_t)kk.y << 32) | kk.x;
+    }
+    const uint32_t toff = own ? s.geo_tri_off + tri * 48u : REF_NONE * 64u;
+    const float4 c0 = geo_load(geo, toff), c1 = geo_load(geo, toff + 16u), c2 = geo_load(geo, toff + 32u);
+    float tm = tMax0;
+    int hit = hit0;
+    uint64_t after = 0;               // keys <= after are behind the fold
+    bool first = true;
+    for (uint32_t guard = 0; guard <= ncand; ++guard) {
+        float e0, e1, e2, det, ts;
+        const bool pass = own & (first | (ck > after)) & tri_test<false>(r, c0, c1, c2, tm, e0, e1, e2, det, ts);
+        if (__ballot(pass) == 0) break;
+        uint64_t kmin = pass ? ck : ~0ull;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t v = ((uint64_t)(uint32_t)__shfl_xor((int)(kmin >> 32), o) << 32) |
+                               (uint32_t)__shfl_xor((int)(uint32_t)kmin, o);
+            kmin = v < kmin ? v : kmin;
+        }
+        const int j = __ffsll((long long)__ballot(pass & (ck == kmin))) - 1;
+        tm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts * (1.0f / det)), j));
+        hit = __builtin_amdgcn_readlane((int)tri, j);
+        after = kmin;
+        first = false;
     }
     return hit;
 }
@@ -1064,7 +1237,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             if (WF_STATS && done) atomicAdd(&hist[(t.rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (t.rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
-                const uint32_t kind = t.rid >> 30, p = (uint32_t)PT_CHECK(b.fault, t.rid & 0x3fffffffu, b.n, PT_SITE_RESULT);
+                const uint32_t kind = t.rid >> 30, p = (uint32_t)PT_CHECK(b.fault, t.rid & WF_RID_P, b.n, PT_SITE_RESULT);
                 if (kind == 2) b.hit[p] = wf_tri_index<TBL>(t.hitTri);
                 else b.occ[2 * (size_t)p + kind] = t.hitTri != -1 ? 1 : 0;
                 busy = 0;
@@ -1090,17 +1263,9 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     float ntmax;
                     bool nany;
                     wf_load_ray(b, kind, myid, mode, nr, ntmax, nany, p);
-                    float zlo;
-                    uint32_t root = REF_NONE;
-                    int nlt = 0, nlc = 0;
-                    if (box_fast(nr, s.root_min[0], s.root_min[1], s.root_min[2], s.root_max[0], s.root_max[1],
-                                 s.root_max[2], zlo)) {
-                        root = s.root_ref;
-                        if (root & REF_LEAF) { if (TBL) decode_leaf(s, root, nlt, nlc); else nlt = (int)root; root = REF_NONE; }
-                    }
-                    t.r = nr; t.tMax = ntmax; t.rid = (kind << 30) | p;
-                    t.hitTri = -1; t.spa &= WF_SPA_STRIDE - 1u; t.cur = root; t.lt = nlt; t.lc = nlc;
-                    t.nst = 0;
+                    t.r = nr;
+                    wf_ray_start<TBL>(s, t, ntmax);
+                    t.rid = (kind << 30) | p;
                     busy = 1;
                 }
             }
@@ -1114,30 +1279,45 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         }
         int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
         if (WF_COOP_TAIL && !TBL && !WF_STATS && exhausted) {
-            // the drain: a wave down to one any-hit ray finishes it with all its lanes
+            // the drain: a wave down to one ray finishes it with all its lanes
             if (__popcll(busym) == 1) {
                 const int o = __ffsll((long long)busym) - 1;
                 const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
                 const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
-                if (orid < (2u << 30) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u) {
+                if (!(orid & WF_RID_NOCOOP) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u &&
+                    (WF_COOP_TAIL >= 2 || orid < (2u << 30))) {
                     auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
                     RayP r;
                     r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
                     r.d = mk3(rdf(t.r.d.x), rdf(t.r.d.y), rdf(t.r.d.z));
                     r.inv = mk3(rdf(t.r.inv.x), rdf(t.r.inv.y), rdf(t.r.inv.z));
                     r.perm = __builtin_amdgcn_readlane(t.r.perm, o);
-                    const bool occl = wf_coop_anyhit<STK>(
-                        s, b, geo, lds, r, rdf(t.tMax), (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o),
-                        (uint32_t)__builtin_amdgcn_readlane(t.lt, o), ospa, (ospa & (WF_SPA_STRIDE - 1u)) >> 3);
+                    const uint32_t ocur = (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o);
+                    const uint32_t olt = (uint32_t)__builtin_amdgcn_readlane(t.lt, o);
+                    const uint32_t otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
+                    int res;
+                    if (orid < (2u << 30)) {
+                        res = wf_coop_anyhit<STK>(s, b, geo, lds, r, rdf(t.tMax), ocur, olt, ospa, otl) ? 1 : 0;
+                    } else {
+                        const int h0 = wf_tri_index<false>(__builtin_amdgcn_readlane(t.hitTri, o));
+                        res = wf_coop_closest<STK>(s, geo, lds, b, r, rdf(t.tMax), h0, ocur, olt, ospa, otl);
+                    }
                     if (busy != 0) {
-                        const uint32_t p = (uint32_t)PT_CHECK(b.fault, t.rid & 0x3fffffffu, b.n, PT_SITE_RESULT);
-                        b.occ[2 * (size_t)p + (t.rid >> 30)] = occl ? 1 : 0;
-                        busy = 0;
-                        t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;
+                        const uint32_t kind = t.rid >> 30;
+                        if (res == -2) {         // beyond the cooperative finish's capacity: trace it again, alone
+                            wf_ray_start<TBL>(s, t, kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX);
+                            t.rid |= WF_RID_NOCOOP;
+                        } else {
+                            const uint32_t p = (uint32_t)PT_CHECK(b.fault, t.rid & WF_RID_P, b.n, PT_SITE_RESULT);
+                            if (kind == 2) b.hit[p] = res;
+                            else b.occ[2 * (size_t)p + kind] = (uint8_t)res;
+                            busy = 0;
+                            t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;
+                        }
                     }
                     continue;
                 }
-                thr = 0;                 // a closest-hit ray: step it to the end
+                thr = 0;                 // not for the cooperative finish: step it to the end
             } else {
                 thr = max(thr, 1);       // come back here when one ray is left
             }

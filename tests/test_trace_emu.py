@@ -19,3 +19,6 @@ def test_packed_and_wide_ranges_agree():
     # the wave-cooperative finish of any-hit rays (pt_wf.h wf_coop_anyhit) gives the
     # sequential traversal's occlusion from any hand-over point
     assert "coop rays" in r.stdout and "coop rays 0 " not in r.stdout and " mismatches 0 iterations" in r.stdout
+    # ... and of closest-hit rays (wf_coop_closest: DFS-order keys, the candidates folded in key order)
+    assert "coop closest rays" in r.stdout and "coop closest rays 0 " not in r.stdout
+    assert [ln for ln in r.stdout.splitlines() if ln.startswith("coop closest")][0].split()[5] == "0"

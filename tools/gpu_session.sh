@@ -8,6 +8,7 @@
 #   prof     rocprofv3 --kernel-trace --stats of bench.py --serial and of the default command
 #   census   trace census of these sources -> profiles/census.json (needs the stats variant)
 #   record   profiles/pmc.json from this session's N = 1 bench lines
+#   shard    the multi-GPU share simulation (per-rank rates at N = 1/2/4/8 on one GPU)
 #   tail     WF_TIMING drain census of the lone-frame (D2) trace launches
 #   fuzz     the widened fuzz campaign (SEEDS=40000 random scenes x 3 kernel modes vs the oracle)
 # Output under gpurun_out/$TAG.  Every GPU step has its own time limit; the first failing
@@ -52,6 +53,9 @@ for s in ${STEPS:-smoke tests bench}; do
           --config $c --sync-per-frame --steps 8 --warmup 4 --no-parity --no-pmc --serial-steps 0 > $O/tail_$c.json \
           2> $O/tail_$c.err
       done ;;
+    shard)     # the multi-GPU share simulation: rank 0's rows of an N-way split on one GPU (16-frame calls)
+      step shard env GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python tools/shard_sim.py 30 16 > $O/shard_sim.txt 2>&1
+      cat $O/shard_sim.txt ;;
     fuzz)
       step fuzz env PNRT_FUZZ_SEEDS=${SEEDS:-40000} timeout -k 10 1100 python -u -m pytest tests/test_gpu_fuzz.py -x -q \
         --timeout 300 --timeout-method thread > $O/fuzz.log 2>&1

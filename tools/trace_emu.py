@@ -78,7 +78,7 @@ def trace(o, d, any_hit, packed, stop_after=None):
     stack, steps, trace_states = [], 0, []
     while True:
         if stop_after is not None and steps == stop_after:      # hand the state over (packed only)
-            return None, steps, (cur, lt, list(stack))
+            return None, steps, (cur, lt, list(stack)), tmax, (-1 if hit == -1 else (hit & 0xffffff))
         steps += 1
         assert steps < 100000, "runaway"
         assert len(stack) < 64, "stack overflow"
@@ -154,6 +154,59 @@ def coop(o, d, state, stk=8):
     return False, it, peak
 
 
+def coop_closest(o, d, state, tmax0, hit0, stk=8, delta=1e-4):
+    """pt_wf.h wf_coop_closest: a closest-hit ray finished by the wave.  Phase 1
+    walks the frontier in any order (64 entries at a time), each entry carrying
+    its DFS-order key (rank of the hand-over entry: pending range 0, node 1, stack
+    top 2 ...; then one bit per level below it -- near 0, far 1 -- ended by a
+    sentinel bit; the triangle's place in its leaf in the low 8 bits); a triangle
+    accepted at the relaxed bound E (1 + delta) is a candidate, E the least hit
+    distance found.  Phase 2 folds the candidates in key order from (tmax0, hit0)
+    with the exact test: the reference's sequential result.  Returns
+    (hit, iterations) or (None, iterations) for a restart."""
+    inv = 1.0 / d
+    cur, lt, stack = state
+    cap = (stk + 1) * 32
+    top = 1 << 55
+    fr = [(e, ((2 + len(stack) - 1 - k) << 56) | top) for k, e in enumerate(stack)]
+    if cur != NONE: fr.append((cur, (1 << 56) | top))
+    if lt >= (LEAF | (1 << 24)): fr.append((lt, top))
+    E, cands, it = tmax0, [], 0
+    while fr:
+        it += 1
+        k = 1 if len(fr) + len(cands) > cap - 128 else min(len(fr), 64)
+        take, fr = fr[len(fr) - k:], fr[:len(fr) - k]
+        new, er = [], E * (1 + delta)
+        for f, key in reversed(take):
+            if f >= (LEAF | (1 << 24)):
+                th = tri_hit(o, d, f & 0xffffff, er)
+                if th is not None:
+                    cands.append((key, f & 0xffffff))
+                    E = min(E, th)
+                rest = (f + (1 - (1 << 24))) & 0xffffffff
+                if rest >= (LEAF | (1 << 24)): new.append((rest, key + 1))
+            elif not (f & LEAF):
+                sent = (key & ~0xff) & -(key & ~0xff)
+                if sent <= (1 << 8):
+                    return None, it                      # deeper than the key holds: restart
+                bl, br, rl, rr, ax = node_rec(f, True)
+                rf = d[ax] < 0
+                kl = key - sent + (sent >> 1) if not rf else key + (sent >> 1)     # left child's key
+                kr = key + (sent >> 1) if not rf else key - sent + (sent >> 1)
+                if box_hit(o, inv, bl) and rl != LEAF: new.append((rl, kl))
+                if box_hit(o, inv, br) and rr != LEAF: new.append((rr, kr))
+        fr += new
+        if len(fr) + len(cands) > cap:
+            return None, it
+    # phase 2: the exact fold in DFS order
+    tm, hit = tmax0, hit0
+    for key, tri in sorted(cands):
+        th = tri_hit(o, d, tri, tm)
+        if th is not None:
+            tm, hit = th, tri
+    return hit, it
+
+
 rng = np.random.default_rng(1)
 lo, hi = N[0, :3].astype(np.float64), N[0, 3:6].astype(np.float64)
 mism = 0
@@ -186,4 +239,25 @@ for r in range(NR):
         if cm < 5: print("coop mismatch", r, occ, full[:2], stop)
 print(f"coop rays {len(its)} mismatches {cm} iterations mean {np.mean(its):.1f} vs sequential steps "
       f"{np.mean(seq):.1f}, max frontier {peak}")
-sys.exit(1 if (mism or cm) else 0)
+# the cooperative finish of closest-hit rays: same hand-over points, hit and tMax
+# carried over, the keyed fold must give the sequential traversal's hit
+hm, its2, seq2, rs = 0, [], [], 0
+for r in range(NR):
+    o = lo + (hi - lo) * rng.uniform(0, 1, 3)
+    d = rng.normal(size=3); d /= np.linalg.norm(d)
+    full = trace(o, d, False, True)
+    stop = int(rng.integers(0, max(1, full[1])))
+    st = trace(o, d, False, True, stop_after=stop)
+    if st[0] is not None:
+        continue
+    h, n = coop_closest(o, d, st[2], st[3], st[4])
+    if h is None:
+        rs += 1
+        continue
+    its2.append(n); seq2.append(full[1] - stop)
+    if h != full[0]:
+        hm += 1
+        if hm < 5: print("coop closest mismatch", r, h, full[:2], stop)
+print(f"coop closest rays {len(its2)} mismatches {hm} restarts {rs} iterations mean {np.mean(its2):.1f} vs "
+      f"sequential steps {np.mean(seq2):.1f}")
+sys.exit(1 if (mism or cm or hm) else 0)
