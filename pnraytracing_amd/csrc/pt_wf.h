@@ -1278,9 +1278,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             continue;
         }
         int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
-        if (WF_COOP_TAIL && !TBL && !WF_STATS && exhausted) {
-            // the drain: a wave down to one ray finishes it with all its lanes
-            if (__popcll(busym) == 1) {
+        if (WF_COOP_TAIL && !TBL && !WF_STATS) {
+            // a wave never steps a lone ray while it could refill around it (back here
+            // at one busy lane), and once the queue is exhausted -- the drain -- a
+            // wave down to one ray finishes it with all its lanes
+            if (__popcll(busym) == 1 && exhausted) {
                 const int o = __ffsll((long long)busym) - 1;
                 const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
                 const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
@@ -1319,7 +1321,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 }
                 thr = 0;                 // not for the cooperative finish: step it to the end
             } else {
-                thr = max(thr, 1);       // come back here when one ray is left
+                thr = __popcll(busym) == 1 ? 0 : max(thr, 1);   // come back here when one ray is left
             }
         }
         // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------
