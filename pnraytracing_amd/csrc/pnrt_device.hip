@@ -404,6 +404,11 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
                         const float4* primary, float4* colors, bool alone) {
     WfBufs b = L.b;
     if (b.n > WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: too many paths per batch");
+    // the cooperative finish of closest-hit rays pays where the drain leaves the chip
+    // idle -- a call with nothing else in flight (the reference's loop: D2 sync -19 %);
+    // beside other calls' kernels the wave's 64 lanes on one ray cost more than they
+    // save (C2 -2.3 %), so pipelined calls finish only any-hit rays cooperatively
+    b.coop = alone ? 2u : 1u;
     const dim3 g((unsigned)((b.n + 255) / 256));
     b.wr = L.set[0];
     {   // path state + bounce-0 sampling

@@ -117,6 +117,7 @@ struct WfBufs {
     uint32_t nseg_k;         // setup blocks = segments per kind
     unsigned long long* stats; // WF_STATS builds: traversal step census (8 counters)
     uint32_t* fault;   // the context's fault words (host-mapped, see wf_fault), WF_FAULT_* index
+    uint32_t coop;     // the trace's cooperative finish (WF_COOP_TAIL): 1 any-hit rays, 2 closest-hit rays too
     uint32_t n;        // path slots
     int chunk_frames;
     int tiles_x;
@@ -802,8 +803,8 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // while the frontier holds at most CAP - 128, else one (depth-first: +1 per
 // descent, at most the tree depth < 63 before a leaf), so it never overflows.
 #ifndef WF_COOP_TAIL
-#define WF_COOP_TAIL 1      // 0 off, 1 any-hit rays, 2 any-hit and closest-hit rays (wf_coop_closest)
-#endif
+#define WF_COOP_TAIL 2      // 0 off, 1 any-hit rays, 2 closest-hit rays too (wf_coop_closest) in the
+#endif                      // launches of a call with nothing else in flight (WfBufs::coop; see render_batch)
 template <int STK>
 PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo, uint2* lds, const RayP& r,
                            float tMax, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
@@ -1287,7 +1288,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
                 const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
                 if (!(orid & WF_RID_NOCOOP) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u &&
-                    (WF_COOP_TAIL >= 2 || orid < (2u << 30))) {
+                    ((WF_COOP_TAIL >= 2 && b.coop >= 2) || orid < (2u << 30))) {
                     auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
                     RayP r;
                     r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
