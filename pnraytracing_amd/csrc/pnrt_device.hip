@@ -407,8 +407,8 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
     // the cooperative finish of closest-hit rays pays where the drain leaves the chip
     // idle -- a call with nothing else in flight (the reference's loop: D2 sync -19 %);
     // beside other calls' kernels the wave's 64 lanes on one ray cost more than they
-    // save (C2 -2.3 %), so pipelined calls finish only any-hit rays cooperatively
-    b.coop = alone ? 2u : 1u;
+    // save (C2 -2.3 %), so pipelined calls run the instantiation without it
+    const bool cc = alone && WF_COOP_TAIL >= 2;
     const dim3 g((unsigned)((b.n + 255) / 256));
     b.wr = L.set[0];
     {   // path state + bounce-0 sampling
@@ -425,6 +425,8 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             ProfScope ps(c, PNRT_K_TRACE, st);
             if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)
                 hipLaunchKernelGGL((pt_wf_trace<WF_STACK, true>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
+            else if (cc)
+                hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false, true>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
             else hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
         }
         HIPCHK(c, hipGetLastError());

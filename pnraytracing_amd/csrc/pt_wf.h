@@ -117,7 +117,6 @@ struct WfBufs {
     uint32_t nseg_k;         // setup blocks = segments per kind
     unsigned long long* stats; // WF_STATS builds: traversal step census (8 counters)
     uint32_t* fault;   // the context's fault words (host-mapped, see wf_fault), WF_FAULT_* index
-    uint32_t coop;     // the trace's cooperative finish (WF_COOP_TAIL): 1 any-hit rays, 2 closest-hit rays too
     uint32_t n;        // path slots
     int chunk_frames;
     int tiles_x;
@@ -804,7 +803,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // descent, at most the tree depth < 63 before a leaf), so it never overflows.
 #ifndef WF_COOP_TAIL
 #define WF_COOP_TAIL 2      // 0 off, 1 any-hit rays, 2 closest-hit rays too (wf_coop_closest) in the
-#endif                      // launches of a call with nothing else in flight (WfBufs::coop; see render_batch)
+#endif                      // launches of a call with nothing else in flight (pt_wf_trace<.., CC>, render_batch)
 template <int STK>
 PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo, uint2* lds, const RayP& r,
                            float tMax, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
@@ -1068,7 +1067,10 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 8      // waves per SIMD (64 VGPRs: no SLP packing, one-register stack position)
 #endif
-template <int STK, bool TBL>
+// CC: closest-hit rays get the cooperative finish too (wf_coop_closest) -- its own
+// instantiation, launched for a call with nothing else in flight, so the
+// pipelined launches run code without it (C2 -0.9 % with it compiled in)
+template <int STK, bool TBL, bool CC = false>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[(STK + 1) * WF_TRACE_BLOCK];     // STK depths + the spare one (wf_push)
     // nodes and triangle records through one buffer resource (32-bit offsets)
@@ -1288,7 +1290,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
                 const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
                 if (!(orid & WF_RID_NOCOOP) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u &&
-                    ((WF_COOP_TAIL >= 2 && b.coop >= 2) || orid < (2u << 30))) {
+                    ((WF_COOP_TAIL >= 2 && CC) || orid < (2u << 30))) {
                     auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
                     RayP r;
                     r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
@@ -1299,7 +1301,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     const uint32_t olt = (uint32_t)__builtin_amdgcn_readlane(t.lt, o);
                     const uint32_t otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
                     int res;
-                    if (orid < (2u << 30)) {
+                    if (!CC || orid < (2u << 30)) {
                         res = wf_coop_anyhit<STK>(s, b, geo, lds, r, rdf(t.tMax), ocur, olt, ospa, otl) ? 1 : 0;
                     } else {
                         const int h0 = wf_tri_index<false>(__builtin_amdgcn_readlane(t.hitTri, o));
