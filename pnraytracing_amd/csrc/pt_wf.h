@@ -1181,7 +1181,11 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 ckind = __builtin_amdgcn_readfirstlane(bq_seg[g & 15][2]);
                 return;
             }
-            if (__hip_atomic_load(&bq_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) { exhausted = true; return; }
+            if (__hip_atomic_load(&bq_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                exhausted = true;        // (another wave of the block found the queue empty)
+                if (WF_TIMING) { t_exh = __builtin_amdgcn_s_memrealtime(); witer_exh = witer; }
+                return;
+            }
             uint32_t won = 0;
             if (lane == 0) {
                 uint32_t e = g;
