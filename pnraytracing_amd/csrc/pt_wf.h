@@ -37,11 +37,8 @@
 #define WF_SMALL_CALL_PATHS 5000000   // calls with fewer paths (multi-GPU shares: 2.1M at N = 8, 4.2M at N = 4 with 8-frame calls) use all WF_PIPES sets
 #endif
 #define WF_LIGHT_SCAN PT_LIGHT_SCAN
-#ifndef WF_QREGION
-#define WF_QREGION 0        // 1: XCD-affine queue shards -- shard p holds contiguous image regions (see wf_item)
-#endif
 #ifndef WF_QSHARDS
-#define WF_QSHARDS (WF_QREGION ? 8 : 4)   // dequeue counters (<= 8), one 256-B line apart
+#define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
 #endif
 #ifndef WF_QSTRIDE
 #define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
@@ -135,36 +132,17 @@ struct WfBufs {
 PN_DEV void wf_fault(const WfBufs& b, int kind) {
     __hip_atomic_store(b.fault + kind, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// Queue item of ticket t of counter (shard) p.  Interleaved (WF_QREGION 0): item
-// t * WF_QSHARDS + p.  Regions (WF_QREGION 1): the items are cut into chunks of
-// R = ceil(nseg_k / WF_QSHARDS) consecutive segments -- one WF_QSHARDS-th of the
-// image's tiles of one ray kind -- and shard p serves chunks p, p + QS, ... in
-// order: the region p of each kind, kinds in the sweep order.  A block starts on
-// shard blockIdx % QS, and workgroups are dealt to the 8 XCDs round-robin, so with
-// 8 shards each XCD's L2 serves the rays of one image band until its shard runs
-// dry (then its blocks help the others).  Either way an item's ticket grows with
-// the item, so a shard whose ticket maps beyond the queue is dry.
-PN_DEV uint32_t wf_region(const WfBufs& b) { return (b.nseg_k + WF_QSHARDS - 1) / WF_QSHARDS; }
-PN_DEV uint32_t wf_item(const WfBufs& b, uint32_t t, uint32_t p) {
-    if (!WF_QREGION) return t * WF_QSHARDS + p;
-    const uint32_t R = wf_region(b), c = t / R;
-    return (c * WF_QSHARDS + p) * R + (t - c * R);
-}
 // A setup kernel's block 0 resets the dequeue counters of the trace launch that
 // follows it (the previous trace has completed: stream order).  The shade
-// kernels first check that the previous trace handed out every queue item:
-// counter p must have passed every ticket whose item lies below nseg.
+// kernels first check that the previous trace handed out every queue item: item
+// i is ticket i / WF_QSHARDS of counter i % WF_QSHARDS, so counter p must have
+// passed all ceil((nseg - p) / WF_QSHARDS) tickets below nseg.  (Shards of
+// contiguous image regions, one per XCD, each block starting on its XCD's shard:
+// bit-exact, but C2 -0.5 %, C5 -2.3 %, profiles/r04/s4/tune_ab_xcd_*.)
 PN_DEV void wf_check_drained(const WfBufs& b) {
     if (blockIdx.x == 0 && threadIdx.x < WF_QSHARDS) {
         const uint32_t nseg = 3u * b.nseg_k, p = threadIdx.x;
-        uint32_t need;
-        if (!WF_QREGION) {
-            need = nseg > p ? (nseg - p + WF_QSHARDS - 1) / WF_QSHARDS : 0u;
-        } else {             // whole chunks p, p + QS, ... below nseg, and the part of the last one
-            const uint32_t R = wf_region(b), nch = (nseg + R - 1) / R;
-            const uint32_t k = nch > p ? (nch - p + WF_QSHARDS - 1) / WF_QSHARDS : 0u;
-            need = k ? (k - 1u) * R + min(R, nseg - (p + (k - 1u) * WF_QSHARDS) * R) : 0u;
-        }
+        const uint32_t need = nseg > p ? (nseg - p + WF_QSHARDS - 1) / WF_QSHARDS : 0u;
         if (b.counter[p * WF_QSTRIDE] < need) wf_fault(b, WF_FAULT_DRAIN);
     }
 }
@@ -1146,7 +1124,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             uint32_t t = 0;
             if (lane == 0) t = atomicAdd(b.counter + p * WF_QSTRIDE, 1u);
             t = __builtin_amdgcn_readfirstlane(t);
-            const uint32_t item = wf_item(b, t, p);
+            const uint32_t item = t * WF_QSHARDS + p;
             if (item < nseg) {
                 seg = item;
                 break;

@@ -27,7 +27,6 @@ VARIANTS = {
     "block128": ["-DWF_TRACE_BLOCK=128"],
     "block512": ["-DWF_TRACE_BLOCK=512", "-DWF_TRACE_WAVES=4"],
     "stack12": ["-DWF_STACK=12"],
-    "xcd_regions": ["-DWF_QREGION=1"],
     "tunables": ["-DWF_REFILL_PCT=50", "-DWF_TRACE_GRID_PCT=40", "-DWF_TRACE_GRID_PCT_LARGE=90",
                  "-DWF_MAX_CHUNK_FRAMES=8", "-DWF_QSHARDS=8", "-DWF_KIND_ORDER=0x012"],
 }
