@@ -385,21 +385,29 @@ def launches_per_step_of(k_launches: int, steps: int, excl: dict, kname: str):
     return None
 
 
+L2_HIT_CYC, MISS_CYC = 200.0, 900.0   # MI355X_MICROARCH.md: global_load L2-hit / HBM-miss latency (cycles)
+
+
 def derive_bound(hbm_frac, l2_hit, l2_frac, gather_hit=None):
     """The roof that binds, from the counters: "hbm" (bandwidth) when the kernel's
     fabric traffic reaches half the HBM peak; below that the kernel is bound by
-    the latency of its dependent fetch chains -- "hbm-latency" when most of its
-    node / triangle gathers miss the L2 (a scene beyond the L2s: C5), "l2-latency"
-    when they hit (C2: L1/L2-hit chains).  The gathers' own
-    hit rate (gather_hit: the streamed ray records, read once, miss by nature and
-    are taken out) decides when known, else the kernel's whole L2 hit rate.
-    l2_frac (its own requests against the L2 bandwidth) is reported beside it."""
+    the latency of its dependent fetch chains -- "hbm-latency" when at least a
+    third of that latency is spent on L2 misses (a miss costs ~900 cycles, a hit
+    ~200: a gather miss rate above ~10 %, C5's 4.2M-triangle scene beyond the
+    L2s), "l2-latency" otherwise (C2-C4: L1/L2-hit chains).
+    The gathers' own hit rate (gather_hit: the streamed ray records, read once,
+    miss by nature and are taken out) decides when known, else the kernel's whole
+    L2 hit rate.  l2_frac (its own requests against the L2 bandwidth) is
+    reported beside it."""
     if hbm_frac is None:
         return None
     if hbm_frac >= 0.5:
         return "hbm"
     hit = gather_hit if gather_hit is not None else l2_hit
-    return "hbm-latency" if (hit is not None and hit < 0.6) else "l2-latency"
+    if hit is None:
+        return "l2-latency"
+    miss = (1.0 - hit) * MISS_CYC
+    return "hbm-latency" if miss >= (miss + hit * L2_HIT_CYC) / 3.0 else "l2-latency"
 
 
 def gather_hit_rate(fetch_bytes, streamed_bytes, requested_bytes, rays):
@@ -687,9 +695,10 @@ def main():
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
                                                requested["frac_of_l2"] if requested else None, ghit),
                          "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "
-                                       "else the latency of dependent fetch chains -- hbm-latency if the node / "
-                                       "triangle gathers' L2 hit rate (gather_l2_hit_rate; l2_hit_rate when unknown) "
-                                       "< 0.6, l2-latency otherwise; peak / frac stay against HBM",
+                                       "else the latency of dependent fetch chains -- hbm-latency if L2 misses of the "
+                                       "node / triangle gathers (gather_l2_hit_rate; l2_hit_rate when unknown) take "
+                                       ">= 1/3 of the fetch latency (miss ~900, hit ~200 cycles), l2-latency otherwise; "
+                                       "peak / frac stay against HBM",
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

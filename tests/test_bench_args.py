@@ -54,13 +54,14 @@ def test_launch_count_without_kernel_events():
 
 def test_bound_derived_from_counters():
     b = _bench()
-    assert b.derive_bound(0.13, 0.80, 0.32) == "l2-latency"     # C2: L1/L2-hit chains
-    assert b.derive_bound(0.25, 0.52, 0.30) == "hbm-latency"    # C5: 1 GB scene, half the L2 lookups miss
+    assert b.derive_bound(0.13, 0.95, 0.32) == "l2-latency"     # L1/L2-hit chains
+    assert b.derive_bound(0.25, 0.52, 0.30) == "hbm-latency"    # half the L2 lookups miss
     assert b.derive_bound(0.62, 0.90, 0.30) == "hbm"
     assert b.derive_bound(None, 0.5, 0.3) is None
     # C4: the misses are the streamed ray records, the gathers hit
-    assert b.derive_bound(0.08, 0.36, 0.3, gather_hit=0.9) == "l2-latency"
-    assert b.derive_bound(0.27, 0.9, 0.3, gather_hit=0.4) == "hbm-latency"
+    assert b.derive_bound(0.08, 0.44, 0.3, gather_hit=0.998) == "l2-latency"    # C4 (round 4)
+    assert b.derive_bound(0.15, 0.80, 0.4, gather_hit=0.985) == "l2-latency"    # C2
+    assert b.derive_bound(0.28, 0.51, 0.36, gather_hit=0.878) == "hbm-latency"  # C5: 12 % of its gathers miss
     g = b.gather_hit_rate(fetch_bytes=1.0e9, streamed_bytes=1.2e9, requested_bytes=9.0e9, rays=25e6)
     assert abs(g - (1 - 0.4e9 / 8.1e9)) < 1e-9
 
