@@ -691,7 +691,7 @@ def main():
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "iters_per_call": ipc,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
-                       "kernel": kfull},
+                       "kernel": kfull, "calls": "serial" if args.serial else "pipelined"},
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
                                                requested["frac_of_l2"] if requested else None, ghit),
                          "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "

@@ -9,7 +9,10 @@ every launch AND the launches after that first call.  With `--serial --warmup 4
 --steps 8` every call is a whole 16-frame call in flight alone, so the trace
 kernel's average over the later launches is the line's exclusive kernel_ms.
 
-    python tools/prof_summary.py KERNEL_TRACE.csv BENCH_LINE.json [OUT.json]
+    python tools/prof_summary.py KERNEL_TRACE.csv BENCH_LINE.json [OUT.json] [--serial]
+
+The line's config.calls ("serial" / "pipelined", round 4) picks the comparison;
+--serial marks a line written before that field existed.
 """
 import csv
 import json
@@ -21,7 +24,8 @@ SHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": 
 
 
 def main():
-    trace, line_path = sys.argv[1], sys.argv[2]
+    pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+    trace, line_path = pos[0], pos[1]
     line = [json.loads(x) for x in open(line_path) if x.startswith("{")][-1]
     ipc = line["config"]["iters_per_call"]
     rows = []
@@ -30,8 +34,11 @@ def main():
         if name in SHORT:
             rows.append((int(r["Start_Timestamp"]), SHORT[name], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
     rows.sort()
-    prim = [i for i, (_, k, _) in enumerate(rows) if k == "primary"]
-    cut = prim[1] if len(prim) > 1 else 0          # the sizing call ends where the second call's primary pass starts
+    # the sizing call ends where the second call's ray generation starts (one gen
+    # launch per call at these sizes; the primary pass runs only when a pipe's
+    # cached primary records are stale, round 4)
+    gen = [i for i, (_, k, _) in enumerate(rows) if k == "gen"]
+    cut = gen[1] if len(gen) > 1 else 0
     out = {"trace_csv": trace, "bench_line": line_path, "sizing_call_launches": cut, "kernels": {}}
     for k in sorted(set(k for _, k, _ in rows)):
         allv = [d for _, kk, d in rows if kk == k]
@@ -46,14 +53,15 @@ def main():
     # a --serial command's launches are exclusive (compare with kernel_ms); a default
     # command's overlap the other calls' kernels (compare with kernel_ms_pipelined,
     # the HIP-event average over its timed launches)
-    serial = "--serial" in " ".join(sys.argv) or abs((kpipe or 0) - (kms or 0)) < 0.02 * (kms or 1)
+    calls = line["config"].get("calls")
+    serial = calls == "serial" if calls else "--serial" in sys.argv[1:]
     ref = kms if serial else kpipe
     out["check"] = {"kernel": kname, "line_kernel_ms": kms, "line_kernel_ms_pipelined": kpipe,
                     "compared_with": "kernel_ms" if serial else "kernel_ms_pipelined", "rocprof_mean_ms": got,
                     "rel_diff": round(got / ref - 1.0, 4) if (got and ref) else None, "iters_per_call": ipc}
     print(json.dumps(out, indent=1))
-    if len(sys.argv) > 3:
-        json.dump(out, open(sys.argv[3], "w"), indent=1)
+    if len(pos) > 2:
+        json.dump(out, open(pos[2], "w"), indent=1)
 
 
 if __name__ == "__main__":
