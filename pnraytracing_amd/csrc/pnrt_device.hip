@@ -115,6 +115,8 @@ struct pnrt_ctx {
     struct Pipe {
         hipStream_t w = nullptr;
         hipEvent_t ev_join = nullptr, ev_blend = nullptr;
+        hipEvent_t ev_stage = nullptr;   // WF_STAGGER: the call has reached its drain-heavy end
+        bool stage_set = false;
         float4* primary = nullptr;  size_t primary_cap = 0;
         PrimKey prim;
         float4* colors = nullptr;   size_t colors_cap = 0;
@@ -283,6 +285,12 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #ifndef WF_TRACE_PATHS_PER_BLOCK
 #define WF_TRACE_PATHS_PER_BLOCK (8 * WF_TRACE_BLOCK) // > 0: trace grid <= paths / this (small multi-GPU shares)
 #endif
+#ifndef WF_STAGGER
+#define WF_STAGGER 3        // k > 0: calls of >= WF_STAGGER_PATHS paths run on two pipes with the full trace
+#endif                      // grid, each starting when the previous one is k trace / shade launches from its end
+#ifndef WF_STAGGER_PATHS
+#define WF_STAGGER_PATHS 12000000   // (1080p calls of >= 6 frames; a rank's share at N = 2 with 16-frame calls)
+#endif
 #ifndef WF_TRACE_PATHS_PER_BLOCK_ALONE
 #define WF_TRACE_PATHS_PER_BLOCK_ALONE WF_TRACE_BLOCK  // ... for a call with no other call in flight
 #endif
@@ -340,8 +348,8 @@ static WfLayout wf_layout(char* base, size_t n) {
 // other call is in flight (`alone`: an interactive loop that waits for every
 // frame, the reference's own 512x512 one-frame dispatch) has the chip to itself:
 // full occupancy, one block per WF_TRACE_PATHS_PER_BLOCK_ALONE paths.
-static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false) {
-    const unsigned pct = (c->serial || alone) ? 100u : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
+static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false, bool one = false) {
+    const unsigned pct = (c->serial || alone || one) ? 100u : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
     const size_t gmax = (size_t)c->trace_grid * pct / 100;
     const size_t ppb = alone ? WF_TRACE_PATHS_PER_BLOCK_ALONE : WF_TRACE_PATHS_PER_BLOCK;
     return ppb ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + ppb - 1) / ppb)) : (unsigned)gmax;
@@ -401,7 +409,7 @@ static int report_trace_diag(pnrt_ctx* c, const WfBufs& b, hipStream_t st, int b
 // One batch of frames (gen -> {trace -> shade/setup} x depth) on one stream;
 // its colours land in frame slots [0, cf) of `colors`.
 static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, const WfLayout& L, hipStream_t st,
-                        const float4* primary, float4* colors, bool alone) {
+                        const float4* primary, float4* colors, bool alone, bool one, hipEvent_t stage = nullptr) {
     WfBufs b = L.b;
     if (b.n > WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: too many paths per batch");
     // the cooperative finish of closest-hit rays pays where the drain leaves the chip
@@ -416,8 +424,11 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
     }
     HIPCHK(c, hipGetLastError());
-    const unsigned tg = trace_grid_for(c, b.n, alone);
+    const unsigned tg = trace_grid_for(c, b.n, alone, one);
+    // (launch position 2 b: bounce b's trace, 2 b + 1: its shade)
+    const int stage_at = std::max(2 * fp.max_depth - WF_STAGGER, 0);
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
+        if (stage && 2 * bounce == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         // segment dequeue counters: zeroed by the setup kernel that queued the rays
         // (the census builds also clear their words)
         if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 512, st));
@@ -432,6 +443,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         HIPCHK(c, hipGetLastError());
         if (WF_STATS || WF_TIMING)
             if (int rc = report_trace_diag(c, b, st, bounce, tg)) return rc;
+        if (stage && 2 * bounce + 1 == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         {
             ProfScope ps(c, PNRT_K_SHADE, st);
             // MIS + continuation, then the next bounce's sampling (sets alternate)
@@ -444,6 +456,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         }
         HIPCHK(c, hipGetLastError());
     }
+    if (stage && fp.max_depth <= 0) HIPCHK(c, hipEventRecord(stage, st));
     return PNRT_OK;
 }
 
@@ -458,6 +471,7 @@ static int pipes_init(pnrt_ctx* c) {
         HIPCHK(c, hipStreamCreateWithFlags(&P.w, hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&P.ev_blend, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&P.ev_stage, hipEventDisableTiming));
     }
     return PNRT_OK;
 }
@@ -480,13 +494,19 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
     const uint32_t chunk = nf < fit ? nf : fit;
     // calls in flight by call size (paths per batch): small (< 5M: multi-GPU shares)
-    // 4 with > 4 hardware queues; 5M-32M (1080p calls of up to 15 frames) 2 -- their
-    // launches are long enough to fill each other's drains (8-frame calls: C2 +1.8 %,
-    // C3 +2.7 %, C4 +1.6 % against 3); above 32M 3: 4K calls, which hide more of their
-    // HBM-latency-bound traversal (C5 -3.5 % with 2), and the bench's 16-frame 1080p
-    // calls (33.2M paths), for which 2 and 3 measured the same within 1 %
+    // 4 with > 4 hardware queues; 5M-12M 2 -- their launches are long enough to fill
+    // each other's drains (8-frame calls: C2 +1.8 %, C3 +2.7 %, C4 +1.6 % against 3).
+    // From 12M (1080p calls of 6+ frames, 4K calls) the calls are staggered (round 4):
+    // two pipes, the full trace grid, and a call starts only when the previous one
+    // has finished its second-to-last trace launch, so the two overlap just in the
+    // drain-heavy end (last shade / trace / shade / blend) instead of contending for
+    // the chip throughout (same box, 2 rounds: C2 +2.5 %, C3 +3.3 %, C4 +1.2 %, C5
+    // +1.1 %; one call in flight: C2 +1.8 %, C4 -1.8 %).
+    // Without staggering (WF_STAGGER 0): 2 pipes up to 32M, 3 above.
     const size_t call_paths = per_frame * chunk;
-    const unsigned want = c->serial ? 1u
+    const bool stagger = !c->serial && WF_STAGGER > 0 && call_paths >= (size_t)WF_STAGGER_PATHS;
+    const bool one = c->serial || stagger;       // the trace launch may take the whole chip
+    const unsigned want = stagger ? 2u : one ? 1u
                         : call_paths < (size_t)WF_SMALL_CALL_PATHS ? c->n_pipes_small
                         : call_paths < (size_t)WF_HUGE_CALL_PATHS ? WF_PIPES_MEDIUM : WF_PIPES_LARGE;
     const unsigned npipes = std::max(1u, std::min(want, c->n_pipes_small));   // only sets pipes_init made
@@ -497,6 +517,7 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     // A call with nothing in flight stays on the last call's pipe (its buffers are
     // free, its primary records likely still valid, its lines still in the caches);
     // otherwise the calls rotate over the pipes
+    const unsigned prev_pipe = c->last_pipe;
     const unsigned pi = (alone && c->last_pipe < npipes) ? c->last_pipe : c->next_pipe % npipes;
     c->next_pipe = (pi + 1) % npipes;
     c->last_pipe = pi;
@@ -526,6 +547,10 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     hipStream_t w = P.w;
     // this pipe's buffers were last read by the blend of the call that used it last
     if (P.blend_pending) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));
+    // staggered calls: this one starts when the previous one reaches its last bounces
+    if (stagger && prev_pipe != pi && prev_pipe < WF_PIPES && c->pipe[prev_pipe].stage_set)
+        HIPCHK(c, hipStreamWaitEvent(w, c->pipe[prev_pipe].ev_stage, 0));
+    P.stage_set = false;
     // The primary records (camera ray's closest hit per pixel of the shard) depend
     // on the camera, the frame size, the shard, the traversal mode and the scene
     // (scene_epoch: arrays, materials, environment) -- not on the frame number: the
@@ -566,7 +591,10 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         a.b.tiles_x = tiles_x;
         a.b.first_frame = first + f0;
         if (f0) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));   // the previous group's blend has read the colours
-        if ((rc = render_batch(c, s, fp, a, w, P.primary, P.colors, alone))) return rc;
+        const bool last = f0 + cf >= nf;
+        if ((rc = render_batch(c, s, fp, a, w, P.primary, P.colors, alone, one, stagger && last ? P.ev_stage : nullptr)))
+            return rc;
+        if (stagger && last) P.stage_set = true;
         HIPCHK(c, hipEventRecord(P.ev_join, w));
         HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join, 0));
         {   // the blends run in call order on the caller's stream
@@ -659,6 +687,7 @@ void pnrt_destroy(pnrt_ctx* c) {
         if (P.w) (void)hipStreamDestroy(P.w);
         if (P.ev_join) (void)hipEventDestroy(P.ev_join);
         if (P.ev_blend) (void)hipEventDestroy(P.ev_blend);
+        if (P.ev_stage) (void)hipEventDestroy(P.ev_stage);
     }
 
     for (auto& p : c->ev_pending) { c->ev_pool.push_back(p.second.first); c->ev_pool.push_back(p.second.second); }

@@ -8,7 +8,7 @@ product library itself is built by the session fixture.
   guard1 / bounds  build.py DIAG_VARIANTS (tests/test_gpu_fault.py)
   pipes1           one call in flight (the census build's -DWF_PIPES=1)
   tunables         trace block 128 / 512, LDS stack depth 12, refill threshold,
-                   grid caps, frames per batch
+                   grid caps, frames per batch, call staggering off / other points
 """
 import concurrent.futures
 import os
@@ -29,6 +29,8 @@ VARIANTS = {
     "stack12": ["-DWF_STACK=12"],
     "tunables": ["-DWF_REFILL_PCT=50", "-DWF_TRACE_GRID_PCT=40", "-DWF_TRACE_GRID_PCT_LARGE=90",
                  "-DWF_MAX_CHUNK_FRAMES=8", "-DWF_QSHARDS=8", "-DWF_KIND_ORDER=0x012"],
+    "nostagger": ["-DWF_STAGGER=0"],
+    "stagger": ["-DWF_STAGGER=5", "-DWF_STAGGER_PATHS=4000000"],
 }
 
 
