@@ -288,6 +288,9 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #ifndef WF_STAGGER
 #define WF_STAGGER 3        // k > 0: calls of >= WF_STAGGER_PATHS paths run on two pipes with the full trace
 #endif                      // grid, each starting when the previous one is k trace / shade launches from its end
+#ifndef WF_TRACE_GRID_PCT_ONE
+#define WF_TRACE_GRID_PCT_ONE 100   // trace grid of a staggered call, % of full occupancy
+#endif
 #ifndef WF_STAGGER_PATHS
 #define WF_STAGGER_PATHS 12000000   // (1080p calls of >= 6 frames; a rank's share at N = 2 with 16-frame calls)
 #endif
@@ -349,7 +352,7 @@ static WfLayout wf_layout(char* base, size_t n) {
 // frame, the reference's own 512x512 one-frame dispatch) has the chip to itself:
 // full occupancy, one block per WF_TRACE_PATHS_PER_BLOCK_ALONE paths.
 static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false, bool one = false) {
-    const unsigned pct = (c->serial || alone || one) ? 100u : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
+    const unsigned pct = (c->serial || alone) ? 100u : one ? WF_TRACE_GRID_PCT_ONE : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
     const size_t gmax = (size_t)c->trace_grid * pct / 100;
     const size_t ppb = alone ? WF_TRACE_PATHS_PER_BLOCK_ALONE : WF_TRACE_PATHS_PER_BLOCK;
     return ppb ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + ppb - 1) / ppb)) : (unsigned)gmax;

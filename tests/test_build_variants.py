@@ -30,7 +30,7 @@ VARIANTS = {
     "tunables": ["-DWF_REFILL_PCT=50", "-DWF_TRACE_GRID_PCT=40", "-DWF_TRACE_GRID_PCT_LARGE=90",
                  "-DWF_MAX_CHUNK_FRAMES=8", "-DWF_QSHARDS=8", "-DWF_KIND_ORDER=0x012"],
     "nostagger": ["-DWF_STAGGER=0"],
-    "stagger": ["-DWF_STAGGER=5", "-DWF_STAGGER_PATHS=4000000"],
+    "stagger": ["-DWF_STAGGER=5", "-DWF_STAGGER_PATHS=4000000", "-DWF_TRACE_GRID_PCT_ONE=90"],
 }
 
 
