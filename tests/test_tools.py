@@ -22,7 +22,10 @@ def _line(kms, kpipe, traffic=3.2e9, n=1):
 def test_prof_summary_excludes_the_sizing_call(tmp_path):
     rows, t = [], 0
     for call in range(3):                    # sizing call (slow), then two timed calls
-        for k, ms in [("pt_primary_wf", 0.2)] + [("pt_wf_trace<8, false>", 3.4 if call == 0 else 3.0)] * 4:
+        # each call starts with its ray generation; the primary pass runs in the
+        # first call only (its records are reused while the camera stays)
+        prim = [("pt_primary_wf", 0.2)] if call == 0 else []
+        for k, ms in prim + [("pt_wf_gen_setup", 1.8)] + [("pt_wf_trace<8, false>", 3.4 if call == 0 else 3.0)] * 4:
             rows.append({"Kernel_Name": f"void {k}(DevScene)", "Start_Timestamp": t, "End_Timestamp": t + int(ms * 1e6)})
             t += int(ms * 1e6) + 1000
     tr = tmp_path / "trace.csv"
@@ -30,7 +33,9 @@ def test_prof_summary_excludes_the_sizing_call(tmp_path):
         w = csv.DictWriter(f, ["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
         w.writeheader(); w.writerows(rows)
     ln = tmp_path / "line.json"
-    ln.write_text("noise\n" + json.dumps(_line(3.0, 3.0)) + "\n")
+    line = _line(3.0, 3.1)
+    line["config"]["calls"] = "serial"       # a --serial command: compared with the exclusive kernel_ms
+    ln.write_text("noise\n" + json.dumps(line) + "\n")
     out = tmp_path / "out.json"
     subprocess.run([sys.executable, os.path.join(REPO, "tools", "prof_summary.py"), str(tr), str(ln), str(out)],
                    check=True, capture_output=True)
