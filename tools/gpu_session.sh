@@ -3,7 +3,8 @@
 #   smoke    __graft_entry__.smoke()
 #   tests    the whole -m gpu suite (TESTS= to narrow it, e.g. TESTS="tests/test_gpu_parity.py")
 #   bench    bench.py C2 default (live PMC, CPU leg with the parity check)   [CONFIGS= for others]
-#   d2       the reference's dispatch shape D2 / D3, pipelined and synchronised per frame
+#   d2       the reference's dispatch shape D2 / D3, pipelined and synchronised per frame (no HIP events;
+#            + a synchronised run with every kernel timed)
 #   ab       A/B of prebuilt variants (VARIANTS="name ...", ROUNDS=n): C2 (+ AB_CONFIGS) per variant
 #   prof     rocprofv3 --kernel-trace --stats of bench.py --serial and of the default command
 #   census   trace census of these sources -> profiles/census.json (needs the stats variant)
@@ -66,13 +67,17 @@ for s in ${STEPS:-smoke tests bench}; do
         step bench-$c timeout -k 10 600 python bench.py --config $c $extra ${BENCH_ARGS:-} > $O/bench_$c.json 2> $O/bench_$c.err
         summ $O/bench_$c.json
       done ;;
-    d2)
+    d2)        # the headline lines without HIP events (an event pair around each of a frame's 10
+               # launches costs ~12 % of a synchronised 512x512 frame); + one with every kernel timed
       for c in ${DCONFIGS:-D2 D3}; do
         for sync in "" "--sync-per-frame"; do
           step $c$sync timeout -k 10 200 python bench.py --config $c $sync --steps 240 --warmup 16 --no-cpu-baseline \
-            --no-pmc --serial-steps 0 --kernel-times > $O/${c}${sync}.json 2> $O/${c}${sync}.err
+            --no-pmc --serial-steps 0 --no-kernel-events > $O/${c}${sync}.json 2> $O/${c}${sync}.err
           summ $O/${c}${sync}.json
         done
+        step $c-kt timeout -k 10 200 python bench.py --config $c --sync-per-frame --steps 240 --warmup 16 --no-cpu-baseline \
+          --no-pmc --serial-steps 0 --kernel-times > $O/${c}--sync-per-frame-kernel-times.json 2> $O/${c}-kt.err
+        summ $O/${c}--sync-per-frame-kernel-times.json
       done ;;
     ab)
       for r in $(seq 1 ${ROUNDS:-2}); do
