@@ -498,7 +498,8 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     const uint32_t chunk = nf < fit ? nf : fit;
     // calls in flight by call size (paths per batch): small (< 5M: multi-GPU shares)
     // 4 with > 4 hardware queues; 5M-12M 2 -- their launches are long enough to fill
-    // each other's drains (8-frame calls: C2 +1.8 %, C3 +2.7 %, C4 +1.6 % against 3).
+    // each other's drains (measured on 8-frame 1080p calls before the staggering: C2
+    // +1.8 %, C3 +2.7 %, C4 +1.6 % against 3).
     // From 12M (1080p calls of 6+ frames, 4K calls) the calls are staggered (round 4):
     // two pipes, the full trace grid, and a call starts only when the previous one
     // has finished its second-to-last trace launch, so the two overlap just in the
