@@ -303,7 +303,7 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 // segment counts, dequeue counters + census words (+ the timing builds' stamps).
 static size_t wf_bytes(size_t n) {
     const size_t npad = (n + 255) / 256 * 256, nseg = npad / 256;
-    return 2 * (npad * 16 * 8 + nseg * 4 + 256) + n * (4 + 2) + 256 + npad * 32 + nseg * 12 + 256 + 2048 + 512 +
+    return 2 * (npad * 16 * 8 + nseg * 4 + 256) + n * (4 + 2) + 256 + npad * 32 + nseg * 12 + 256 + WF_COUNTER_BYTES + 512 +
            (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
 }
 // The two path-state sets of a batch (entries are indexed up to npad: a block's
@@ -338,8 +338,8 @@ static WfLayout wf_layout(char* base, size_t n) {
     b.rayD = reinterpret_cast<float4*>(base + off); off += rec;
     b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
     off = (off + 255) & ~(size_t)255;
-    b.counter = reinterpret_cast<unsigned int*>(base + off);               // 8 counters, 256 B apart
-    b.stats = reinterpret_cast<unsigned long long*>(base + off + 2048);
+    b.counter = reinterpret_cast<unsigned int*>(base + off);               // WF_QSHARDS counters, WF_QSTRIDE dwords apart
+    b.stats = reinterpret_cast<unsigned long long*>(base + off + WF_COUNTER_BYTES);
     b.n = (uint32_t)n;
     return L;
 }
@@ -434,7 +434,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (stage && 2 * bounce == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         // segment dequeue counters: zeroed by the setup kernel that queued the rays
         // (the census builds also clear their words)
-        if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, 2048 + 512, st));
+        if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)

@@ -38,11 +38,13 @@
 #endif
 #define WF_LIGHT_SCAN PT_LIGHT_SCAN
 #ifndef WF_QSHARDS
-#define WF_QSHARDS 4        // dequeue counters (<= 8), one 256-B line apart
+#define WF_QSHARDS 16       // dequeue counters, one 128-B line apart
 #endif
 #ifndef WF_QSTRIDE
-#define WF_QSTRIDE 64       // dwords between dequeue counters (one 256-B line each)
+#define WF_QSTRIDE 32       // dwords between dequeue counters (one 128-B line each)
 #endif
+// bytes of the dequeue-counter area (the census / timing words follow it)
+#define WF_COUNTER_BYTES (WF_QSHARDS * WF_QSTRIDE * 4 > 2048 ? WF_QSHARDS * WF_QSTRIDE * 4 : 2048)
 #ifndef WF_TRACE_BLOCK
 #define WF_TRACE_BLOCK 256   // trace workgroup size (128, 256 or 512)
 #endif
