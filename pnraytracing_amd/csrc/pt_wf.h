@@ -140,7 +140,7 @@ PN_DEV void wf_fault(const WfBufs& b, int kind) {
 // i is ticket i / WF_QSHARDS of counter i % WF_QSHARDS, so counter p must have
 // passed all ceil((nseg - p) / WF_QSHARDS) tickets below nseg.  (Shards of
 // contiguous image regions, one per XCD, each block starting on its XCD's shard:
-// bit-exact, but C2 -0.5 %, C5 -2.3 %, profiles/r04/s4/tune_ab_xcd_*.)
+// bit-exact, but C2 -0.5 %, C5 -2.3 %, profiles/r04/s4/summary.txt.)
 PN_DEV void wf_check_drained(const WfBufs& b) {
     if (blockIdx.x == 0 && threadIdx.x < WF_QSHARDS) {
         const uint32_t nseg = 3u * b.nseg_k, p = threadIdx.x;
