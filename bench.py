@@ -13,7 +13,14 @@ reference's OBJ assets do not exist), the reference's real 1k HDR.
 N > 1: one process per GPU; the image rows are dealt in 8-row bands
 (rank r owns bands b with b % N == r), each rank renders its rows, and the
 accumulated rows are gathered to rank 0 over RCCL every step (strong
-scaling: the frame is fixed, its rows are split).
+scaling: the frame is fixed, its rows are split).  `bench.py --gpus N` run
+directly (no WORLD_SIZE in the environment) launches its own N ranks: the
+parent never touches the GPU, starts `torch.distributed.run --nproc-per-node N`
+as a child process, relays rank 0's line and exits with the worst rank's exit
+code; with --backend nccl and fewer than N visible GPUs it exits non-zero
+before anything runs (never a 1-GPU line under --gpus N).  Rank 0 runs the live
+PMC passes over its own share of the rows before it initialises the GPU, so
+an N > 1 line carries live traffic too.
 
 Prints ONE JSON line (rank 0).  Roofline of the dominant kernel (pt_wf_trace),
 every figure measured by this run:
@@ -79,7 +86,7 @@ KSHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup":
           "pt_primary_kernel": "primary", "pt_primary_wf": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -119,7 +126,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo = host-staged rehearsal)")
     ap.add_argument("--child", action="store_true", help=argparse.SUPPRESS)   # a PMC pass's workload: no output
-    return ap.parse_args()
+    ap.add_argument("--shard-world", type=int, default=1, help=argparse.SUPPRESS)   # child: rank 0's share of N
+    return ap.parse_args(argv)
 
 
 def log(*a):
@@ -159,9 +167,10 @@ def _read_counters(d):
     return out
 
 
-def live_pmc(args):
+def live_pmc(args, shard_world: int = 1):
     """Two rocprofv3 --kernel-trace --pmc passes over a short run of this same
-    workload (child processes: this process has not touched the GPU yet).
+    workload (child processes: this process has not touched the GPU yet) -- at
+    N > 1 over rank 0's share of an N-way split (shard_world), rendered alone.
     Returns {class: {"bytes_per_launch", "launches_per_step", "l2_hit_rate"}}
     or None when rocprofv3 is absent or a pass fails."""
     exe = shutil.which("rocprofv3")
@@ -186,7 +195,7 @@ def live_pmc(args):
                    "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
             if args.spp:
                 cmd += ["--spp", str(args.spp)]
-            cmd += ["--iters-per-call", str(args.iters_per_call)]
+            cmd += ["--iters-per-call", str(args.iters_per_call), "--shard-world", str(shard_world)]
             log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
             t = time.perf_counter()
             with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
@@ -422,14 +431,128 @@ def gather_hit_rate(fetch_bytes, streamed_bytes, requested_bytes, rays):
     return max(0.0, min(1.0, 1.0 - (fetch_bytes - streamed_bytes / 2.0) / req))
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+# ---- self-launch of N ranks (bench.py --gpus N without a launcher) ------------------------------
+RC_DIR_ENV = "PNRT_BENCH_RC_DIR"     # the self-launch's directory of per-rank exit codes
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_launch_cmd(n: int, port: int, argv) -> list:
+    """torch.distributed.run over this script with the same arguments (one rank per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def worst_exit_code(codes: dict, n: int, launcher_rc: int) -> int:
+    """The worst (largest) exit code over the N ranks; a rank that left no code
+    (killed, crashed before recording) counts as the launcher's code, at least 1."""
+    worst = max(codes.values()) if codes else 0
+    if len(codes) < n or (launcher_rc != 0 and worst == 0):
+        worst = max(worst, launcher_rc if launcher_rc > 0 else 1)
+    return worst
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 and no WORLD_SIZE: start N ranks of this script as a CHILD
+    torch.distributed.run (never an exec: a process that has touched the GPU must
+    not replace itself, and this one never touches it -- device_count() does not
+    initialise HIP on this image).  Rank 0's JSON line reaches stdout through the
+    inherited descriptor; the return value is the worst rank's exit code."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} with --backend nccl needs one GPU per rank, but {ndev} GPU(s) are "
+              f"visible; no line is printed (a 1-GPU line under --gpus {args.gpus} would be wrong).  Use "
+              f"--backend gloo to rehearse {args.gpus} ranks on fewer GPUs.", file=sys.stderr, flush=True)
+        return 2
+    if ndev == 0:
+        print("bench.py: no GPU visible", file=sys.stderr, flush=True)
+        return 2
+    rc_dir = tempfile.mkdtemp(prefix="pnrt_bench_rc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env[RC_DIR_ENV] = rc_dir
+    cmd = rank_launch_cmd(args.gpus, free_port(), argv)
+    log(f"launching {args.gpus} ranks ({args.backend}): {' '.join(cmd[1:6])} ...")
+    try:
+        r = subprocess.run(cmd, env=env)
+        codes = {}
+        for f in os.listdir(rc_dir):
+            if f.startswith("rc."):
+                try:
+                    codes[int(f[3:])] = int(open(os.path.join(rc_dir, f)).read().strip())
+                except ValueError:
+                    pass
+    finally:
+        shutil.rmtree(rc_dir, ignore_errors=True)
+    rc = worst_exit_code(codes, args.gpus, r.returncode)
+    if rc:
+        log(f"rank exit codes {dict(sorted(codes.items()))}, launcher {r.returncode}: exit {rc}")
+    return rc
+
+
+def record_exit_code(rc: int) -> None:
+    """A self-launched rank records its exit code for the parent (launch_ranks)."""
+    d = os.environ.get(RC_DIR_ENV)
+    if d and os.path.isdir(d):
+        with open(os.path.join(d, f"rc.{os.environ.get('RANK', '0')}"), "w") as f:
+            f.write(str(int(rc)))
+
+
+def step_rooflines(pmc, excl, ms_per_step):
+    """The whole step against the HBM roof (VERDICT r4 "Next" 5): the fabric bytes
+    of every kernel of a step (PMC, 2 x FETCH_SIZE + WRITE_SIZE per launch -- exact
+    for the streamed path state, an upper bound for gathers) over the step's
+    wall time; and per kernel class (gen, shade, blend, trace) its bytes per launch
+    over its EXCLUSIVE launch time (PNRT_SERIAL steps), with the [1x, 2x]
+    FETCH_SIZE bounds as frac_bounds.  (The dominant kernel's calibrated figure
+    is roofline.frac.)  Returns (step, {class: ...}) or (None, None)."""
+    if not pmc:
+        return None, None
+    tot = sum(e["bytes_per_launch"] * e["launches_per_step"] for e in pmc.values())
+    step = {"bytes_per_step": round(tot), "ms_per_step": round(ms_per_step, 4),
+            "achieved": round(tot / (ms_per_step * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(tot / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "counting": f"sum over the step's launches of {STREAM_FACTOR:g} x FETCH_SIZE + WRITE_SIZE "
+                        f"(live PMC) / the timed ms_per_step (pipelined calls overlap: whole-step rate)"}
+    per = {}
+    for k, e in pmc.items():
+        ms = (excl.get(k) or {}).get("ms_per_launch")
+        if not ms:
+            continue
+        lo = GATHER_FACTOR * e["fetch_bytes"] + e["write_bytes"]
+        hi = e["bytes_per_launch"]
+        per[k] = {"traffic": round(hi), "kernel_ms": ms, "achieved": round(hi / (ms * 1e-3) / 1e9, 2),
+                  "frac": round(hi / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                  "frac_bounds": [round(lo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  round(hi / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)],
+                  "launches_per_step": round(e["launches_per_step"], 3),
+                  "l2_hit_rate": round(e["l2_hit_rate"], 4) if "l2_hit_rate" in e else None}
+    return step, (per or None)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None and not args.child:
+        sys.exit(launch_ranks(args, argv))
+    world = int(world_env or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not args.child:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: the line would not measure "
+                         f"--gpus {args.gpus} ranks")
     # live PMC first, while this process has not initialised the GPU (the passes are
-    # child processes under rocprofv3)
+    # child processes under rocprofv3); at N > 1 rank 0 profiles its own share before
+    # it joins the process group (the other ranks wait there)
     pmc = None
-    if world == 1 and not args.child and not args.no_pmc:
-        pmc = live_pmc(args)
+    if rank == 0 and not args.child and not args.no_pmc:
+        pmc = live_pmc(args, shard_world=world)
     if world > 1:
         # multi-rank: RCCL adds a stream of its own beside the library's four (own +
         # three workers); 8 hardware queues keep it off theirs (set before HIP starts)
@@ -437,10 +560,6 @@ def main():
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0 and not args.child:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     ndev = torch.cuda.device_count()
     if ndev and local >= ndev:          # rehearsal of N ranks on fewer GPUs (gloo only)
         if args.backend == "nccl":
@@ -487,7 +606,8 @@ def main():
     info = pt.device_info()
     version = pt.version()
 
-    sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local))   # pnraytracing_amd/dist.py
+    sf = ShardedFrame(pt, band=BAND, device=torch.device("cuda", local),   # pnraytracing_amd/dist.py
+                      shard=(args.shard_world, 0) if (args.child and args.shard_world > 1) else None)
     image = None
 
     # every rank plans its calls from the LARGEST share, so all issue the same gathers
@@ -677,6 +797,7 @@ def main():
                       "frac_le_1": (achieved / HBM_PEAK_GBS <= 1.0) if achieved else None}
         kernels = {k: {"ms_per_launch": round(ms / n, 4), "launches_per_step": n / args.steps}
                    for k, (ms, n) in prof.items() if n}
+        step_roof, kernel_roofs = step_rooflines(pmc, excl, elapsed / args.steps * 1e3)
         kfull = {"v1": "pt_render_kernel", "v3": "pt_wf_trace"}[args.kernel]
         line = {
             "metric": "Msamples/sec (whole node) at 1920x1080, 4spp/iter; fraction of HBM roofline",
@@ -691,7 +812,11 @@ def main():
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "iters_per_call": ipc,
                        "traverse": args.mode, "kernel_version": args.kernel, "parallelism": f"row-bands{BAND}x{world}",
-                       "kernel": kfull, "calls": "serial" if args.serial else "pipelined"},
+                       "kernel": kfull, "calls": "serial" if args.serial else "pipelined",
+                       "primary": ("reused across calls (camera fixed): each pipe keeps its primary records while "
+                                   "camera / frame / shard / mode / scene are unchanged, so the timed steps trace "
+                                   "no primary pass (exact: no camera jitter, ray_tracing.comp:980; DESIGN.md "
+                                   "section 15)")},
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
                                                requested["frac_of_l2"] if requested else None, ghit),
                          "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "
@@ -711,7 +836,9 @@ def main():
                          "launches_per_step": launches_per_step,
                          "checks": checks,
                          "requested": requested,
-                         "reference_bytes_per_launch": ref_bytes},
+                         "reference_bytes_per_launch": ref_bytes,
+                         "step": step_roof,
+                         "kernels": kernel_roofs},
             "kernels": kernels,
             "kernels_exclusive": excl or None,
             "fabric_traffic": step_traffic,
@@ -733,4 +860,12 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    _rc = 1
+    try:
+        main()
+        _rc = 0
+    except SystemExit as _e:
+        _rc = _e.code if isinstance(_e.code, int) else (0 if _e.code is None else 1)
+        raise
+    finally:
+        record_exit_code(_rc)

@@ -81,8 +81,14 @@ def build_device(force=False, extra=()):
 #           queued rays go untraced: pnrt_* must report PNRT_E_TRACE
 #   bounds  every fetch / store index of the integrator kernels checked against its
 #           array (pt_diag.h WF_DIAG_BOUNDS): a violation is reported as PNRT_E_TRACE
+#   coop    every ray handed to the cooperative finish after a hash-chosen 0..24 lane
+#           steps (pt_diag.h WF_DIAG_COOP), with the bounds checks: same images
+#   coopsmall  the same with the finishes' limits shrunk (WF_DIAG_COOP_SMALL), so the
+#           closest-hit restart (-2) and the one-entry depth-first regime run routinely
 DIAG_VARIANTS = {"guard1": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_GUARD=1"],
-                 "bounds": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_BOUNDS=1"]}
+                 "bounds": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_BOUNDS=1"],
+                 "coop": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_COOP=24", "-DWF_DIAG_BOUNDS=1"],
+                 "coopsmall": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_COOP=24", "-DWF_DIAG_COOP_SMALL=1", "-DWF_DIAG_BOUNDS=1"]}
 
 
 def variant_path(name: str) -> str:

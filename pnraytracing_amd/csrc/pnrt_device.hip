@@ -74,6 +74,7 @@ struct pnrt_ctx {
     int max_depth = 0, n_interior = 0, root_is_leaf = 0;
     int64_t scene_bytes = 0;
     std::vector<int> light_mat;            // material of each light record's triangle (pnrt_update_materials)
+    std::vector<float4> light_rec_host;    // host copy of the light records (patched, then one upload)
     // env + textures
     void* hdr = nullptr;
     void* rnd = nullptr;
@@ -163,7 +164,7 @@ static int check_fault(pnrt_ctx* c) {
             "diagnostic bounds check: a fetch / store index out of range at site "};
         static const char* site[] = {"?", "node", "triangle", "leaf table", "stack spill", "trace result", "ray record",
                                      "hit attributes", "light record", "env footprint", "albedo texel", "primary record",
-                                     "colour", "path state", "segment"};
+                                     "colour", "path state", "segment", "cooperative frontier"};
         std::string m;
         for (int k = 0; k < WF_FAULT_WORDS; ++k) {
             const uint32_t v = __atomic_load_n(c->fault_host + k, __ATOMIC_ACQUIRE);
@@ -392,6 +393,12 @@ static int report_trace_diag(pnrt_ctx* c, const WfBufs& b, hipStream_t st, int b
         }
         fprintf(stderr, "\n");
     }
+    if (WF_DIAG_COOP) {   // cooperative-finish hand-overs of the launch (tests/test_gpu_coop.py)
+        unsigned long long cc[3];
+        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipMemcpy(cc, b.stats, sizeof cc, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[coop] bounce %d n=%u anyhit=%llu closest=%llu restarts=%llu\n", bounce, b.n, cc[0], cc[1], cc[2]);
+    }
     if (WF_STATS) {
         unsigned long long stt[8 + 48];
         HIPCHK(c, hipStreamSynchronize(st));
@@ -434,7 +441,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (stage && 2 * bounce == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         // segment dequeue counters: zeroed by the setup kernel that queued the rays
         // (the census builds also clear their words)
-        if (WF_STATS || WF_TIMING) HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + 512, st));
+        if (WF_STATS || WF_TIMING || WF_DIAG_COOP) HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)
@@ -444,7 +451,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             else hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
         }
         HIPCHK(c, hipGetLastError());
-        if (WF_STATS || WF_TIMING)
+        if (WF_STATS || WF_TIMING || WF_DIAG_COOP)
             if (int rc = report_trace_diag(c, b, st, bounce, tg)) return rc;
         if (stage && 2 * bounce + 1 == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         {
@@ -889,6 +896,7 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         lrec[7 * (size_t)e + 6] = make_float4(em[0], em[1], em[2], 0.f);
         c->light_mat[e] = mat;
     }
+    c->light_rec_host = lrec;
 
     DevScene& s = c->scene;
     int rc;
@@ -954,14 +962,22 @@ int pnrt_update_materials(pnrt_ctx* c, int first, int count, const float* rec) {
     HIPCHK(c, sync_all(c));
     HIPCHK(c, hipMemcpy(const_cast<float*>(c->scene.materials) + 18 * (size_t)first, rec, 18 * sizeof(float) * (size_t)count,
                         hipMemcpyHostToDevice));
-    // light records carry a copy of their triangle's emission (upload_scene)
+    // light records carry a copy of their triangle's emission (upload_scene): patched
+    // in the host copy, then the span of changed records goes up in ONE copy (an
+    // emissive mesh of thousands of light triangles sharing one material is one
+    // transfer per edit, as the reference's single glTexSubImage1D)
+    size_t lo = c->light_mat.size(), hi = 0;
     for (size_t e = 0; e < c->light_mat.size(); ++e) {
         const int m = c->light_mat[e];
         if (m < first || m >= first + count) continue;
         const float* em = rec + 18 * (size_t)(m - first);
-        const float4 v = make_float4(em[0], em[1], em[2], 0.f);
-        HIPCHK(c, hipMemcpy(const_cast<float4*>(c->scene.light_rec) + 7 * e + 6, &v, sizeof v, hipMemcpyHostToDevice));
+        c->light_rec_host[7 * e + 6] = make_float4(em[0], em[1], em[2], 0.f);
+        lo = std::min(lo, e);
+        hi = e + 1;
     }
+    if (lo < hi)
+        HIPCHK(c, hipMemcpy(const_cast<float4*>(c->scene.light_rec) + 7 * lo, c->light_rec_host.data() + 7 * lo,
+                            (hi - lo) * 7 * sizeof(float4), hipMemcpyHostToDevice));
     ++c->scene_epoch;                    // primary records hold the hit material's emission
     return PNRT_OK;
 }

@@ -17,6 +17,18 @@
 //                   the index is clamped to 0, so no access leaves its array.  Same
 //                   images when nothing trips.  PNRT_DIAG_FORCE_OOB=1 in the
 //                   environment makes one gen fetch out of range (the check's test)
+//   WF_DIAG_COOP    k > 0: every ray of every trace launch (any-hit and closest-hit)
+//                   is handed to the cooperative finish (pt_wf.h wf_coop_anyhit /
+//                   wf_coop_closest) after a hash-chosen 0..k lane steps, whatever the
+//                   wave's busy count -- the product library reaches it only at a
+//                   drained wave's last ray.  The frontier gets an LDS area of its own
+//                   (the other lanes' stacks stay intact).  Same images: the finishes
+//                   are exact.  Hand-overs and restarts are counted per launch and
+//                   printed ("[coop]" lines on stderr)
+//   WF_DIAG_COOP_SMALL  with WF_DIAG_COOP: the finishes' limits shrunk -- the one-entry
+//                   depth-first regime above 8 frontier entries, at most 2 closest-hit
+//                   candidates, keys at most 12 levels below the hand-over -- so the
+//                   -2 restart (the ray traced again by its own lane) happens routinely
 // The measured-and-dropped variants and the knockouts of rounds 1-3 (DESIGN.md
 // section 8) live in git history, not here.
 #pragma once
@@ -32,10 +44,19 @@
 #ifndef WF_DIAG_BOUNDS
 #define WF_DIAG_BOUNDS 0
 #endif
+#ifndef WF_DIAG_COOP
+#define WF_DIAG_COOP 0
+#endif
+#ifndef WF_DIAG_COOP_SMALL
+#define WF_DIAG_COOP_SMALL 0
+#endif
 #if WF_DIAG_GUARD && !defined(PNRT_DIAG_BUILD)
 #error "result-changing diagnostic switches need -DPNRT_DIAG_BUILD (measurement builds only)"
 #endif
-#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS)
+#if (WF_DIAG_COOP || WF_DIAG_COOP_SMALL) && !defined(PNRT_DIAG_BUILD)
+#error "WF_DIAG_COOP builds are diagnostic builds: add -DPNRT_DIAG_BUILD"
+#endif
+#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS || WF_DIAG_COOP)
 
 // Fault words (the context's host-mapped fault area, see pt_wf.h wf_fault)
 #define WF_FAULT_GUARD 0     // a bounded wait of the block-level ray queue ran out (diagnostic builds)
@@ -60,5 +81,5 @@ PN_DEV long long pt_check_bound(uint32_t* fault, long long idx, long long n, int
 enum PtSite {
     PT_SITE_NODE = 1, PT_SITE_TRI, PT_SITE_LEAF_TABLE, PT_SITE_SPILL, PT_SITE_RESULT, PT_SITE_RAY,
     PT_SITE_HIT_ATTR, PT_SITE_LIGHT_REC, PT_SITE_ENV_QUAD, PT_SITE_TEXEL, PT_SITE_PRIMARY, PT_SITE_COLOR,
-    PT_SITE_PATH, PT_SITE_SEGMENT
+    PT_SITE_PATH, PT_SITE_SEGMENT, PT_SITE_COOP
 };

@@ -808,13 +808,30 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 #ifndef WF_COOP_TAIL
 #define WF_COOP_TAIL 2      // 0 off, 1 any-hit rays, 2 closest-hit rays too (wf_coop_closest) in the
 #endif                      // launches of a call with nothing else in flight (pt_wf_trace<.., CC>, render_batch)
+// The finishes' limits (pt_diag.h WF_DIAG_COOP_SMALL shrinks them so the fallbacks run):
+// the frontier size above which one entry per iteration is taken (depth-first), the
+// closest-hit candidates the fold takes (at most a wave), the key's sentinel bit
+#if WF_DIAG_COOP_SMALL
+#define WF_COOP_WIDE(cap) 8u
+#define WF_COOP_MAXCAND 2u
+#define WF_COOP_KEYTOP 20
+#else
+#define WF_COOP_WIDE(cap) ((cap) - 128u)
+#define WF_COOP_MAXCAND 64u
+#define WF_COOP_KEYTOP 55
+#endif
+// The owner's stack lives in `lds` (its slots, depth d at d * stride + 8 * otl, and the
+// spill area); the frontier is built in the wave's slots of `fr` -- the same area as
+// `lds` in the product library (every other lane of the wave is idle then), an area of
+// its own in WF_DIAG_COOP builds (other lanes still trace).
 template <int STK>
-PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo, uint2* lds, const RayP& r,
-                           float tMax, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
+PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_rsrc_t geo, const uint2* lds, uint2* fr,
+                           const RayP& r, float tMax, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     constexpr uint32_t CAP = (STK + 1) * 64u;
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
     auto slot = [&](uint32_t e) -> uint32_t {      // LDS byte address of frontier entry e
+        e = (uint32_t)PT_CHECK(b.fault, e, CAP, PT_SITE_COOP);
         return (e >> 6) * WF_SPA_STRIDE + 8u * (wbase + (e & 63u));
     };
     const float tmc = tMax * 1.000001f;
@@ -828,6 +845,7 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
         if (lane < (uint32_t)STK) {
             e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
         } else {
+            (void)PT_CHECK(b.fault, lane - (uint32_t)STK, b.ovf_stride, PT_SITE_SPILL);
             const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
             e = make_uint2(v.x, v.y);
         }
@@ -839,14 +857,14 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
                        ((lane == sp + 1) & ((uint32_t)lt >= (REF_LEAF | (1u << 24))));
     uint64_t m = __ballot(valid);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // every read of the owner's slots before the writes
-    if (valid) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(lanes_below(m))) = e;
+    if (valid) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(fr) + slot(lanes_below(m))) = e;
     uint32_t size = (uint32_t)__popcll(m);
     bool hit = false;
     while (size > 0) {
-        const uint32_t k = size > CAP - 128u ? 1u : min(size, 64u);
+        const uint32_t k = size > WF_COOP_WIDE(CAP) ? 1u : min(size, 64u);
         const bool mine = lane < k;
         uint2 f = make_uint2(REF_NONE, 0u);
-        if (mine) f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + slot(size - 1u - lane));
+        if (mine) f = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(fr) + slot(size - 1u - lane));
         size -= k;
         // an entry's z: a pushed far child's z-slab lower end, culled as wf_pop culls it
         const bool take = mine & (f.x != REF_NONE) & !(cull & (__uint_as_float(f.y) > zc));
@@ -873,8 +891,8 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
         if (__ballot(acc) != 0) { hit = true; break; }
         const uint64_t bA = __ballot(cA), bB = __ballot(cB);
         const uint32_t base = size + lanes_below(bA) + lanes_below(bB);
-        if (cA) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(base)) = eA;
-        if (cB) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(lds) + slot(base + (cA ? 1u : 0u))) = eB;
+        if (cA) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(fr) + slot(base)) = eA;
+        if (cB) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(fr) + slot(base + (cA ? 1u : 0u))) = eB;
         size += (uint32_t)(__popcll(bA) + __popcll(bB));
     }
     return hit;
@@ -906,20 +924,21 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
 // candidates beyond the capacity, returns -2 and the ray is traced again from
 // its start by its own lane (WF_RID_NOCOOP; rare, exact either way).
 template <int STK>
-PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, uint2* lds, const WfBufs& b, const RayP& r,
-                           float tMax0, int hit0, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
+PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const uint2* lds, uint2* fr, const WfBufs& b,
+                           const RayP& r, float tMax0, int hit0, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     constexpr uint32_t CAP = (STK + 1) * 32u;           // 16-B entries: (ref, z) + key
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
-    auto at = [&](uint32_t i) -> char* {                 // the wave's i-th 8-B LDS slot
-        return reinterpret_cast<char*>(lds) + (i >> 6) * WF_SPA_STRIDE + 8u * (wbase + (i & 63u));
+    auto at = [&](uint32_t i) -> char* {                 // the wave's i-th 8-B LDS slot of the frontier area
+        i = (uint32_t)PT_CHECK(b.fault, i, 2u * CAP, PT_SITE_COOP);
+        return reinterpret_cast<char*>(fr) + (i >> 6) * WF_SPA_STRIDE + 8u * (wbase + (i & 63u));
     };
     auto put = [&](uint32_t e, uint2 v, uint64_t key) {
         *reinterpret_cast<uint2*>(at(2u * e)) = v;
         *reinterpret_cast<uint2*>(at(2u * e + 1u)) = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     };
     const bool cull = r.cull_ok();
-    const uint64_t TOP = 1ull << 55;
+    const uint64_t TOP = 1ull << WF_COOP_KEYTOP;
     const uint32_t sp = spa >> WF_SPA_SHIFT;
     uint2 e = make_uint2(REF_NONE, 0u);
     uint64_t key = 0;
@@ -928,6 +947,7 @@ PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, uint2*
         if (lane < (uint32_t)STK) {
             e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
         } else {
+            (void)PT_CHECK(b.fault, lane - (uint32_t)STK, b.ovf_stride, PT_SITE_SPILL);
             const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
             e = make_uint2(v.x, v.y);
         }
@@ -944,7 +964,7 @@ PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, uint2*
     float E = tMax0;
     bool fail = false;
     while (size > 0) {
-        const uint32_t k = size + ncand > CAP - 128u ? 1u : min(size, 64u);
+        const uint32_t k = size + ncand > WF_COOP_WIDE(CAP) ? 1u : min(size, 64u);
         const bool mine = lane < k;
         uint2 f = make_uint2(REF_NONE, 0u);
         uint64_t fk = 0;
@@ -1001,7 +1021,7 @@ PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, uint2*
         size += nnew;
         ncand += nc;
     }
-    if (fail || ncand > 64u) return -2;
+    if (fail || ncand > WF_COOP_MAXCAND) return -2;
     // phase 2: the exact fold over the candidates in key (= the reference's) order
     const bool own = lane < ncand;
     uint32_t tri = 0;
@@ -1074,9 +1094,23 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 // CC: closest-hit rays get the cooperative finish too (wf_coop_closest) -- its own
 // instantiation, launched for a call with nothing else in flight, so the
 // pipelined launches run code without it (C2 -0.9 % with it compiled in)
+// WF_DIAG_COOP builds: the lane steps after which a ray is handed to the cooperative
+// finish, 0..WF_DIAG_COOP, a hash of its kind and path entry
+PN_DEV bool wf_coop_due(const TravState& t) {
+    uint32_t h = (t.rid & ~WF_RID_NOCOOP) * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return !(t.rid & WF_RID_NOCOOP) && t.nst >= h % (uint32_t)(WF_DIAG_COOP + 1) &&
+           (t.spa >> WF_SPA_SHIFT) + 2u <= 64u;
+}
 template <int STK, bool TBL, bool CC = false>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[(STK + 1) * WF_TRACE_BLOCK];     // STK depths + the spare one (wf_push)
+    // the cooperative finishes' frontier: the wave's own stack slots (the other lanes
+    // are idle then), an area of its own in WF_DIAG_COOP builds (they are not)
+    __shared__ uint2 lds_coop[WF_DIAG_COOP ? (STK + 1) * WF_TRACE_BLOCK : 1];
+    uint2* const fr = WF_DIAG_COOP ? lds_coop : lds;
     // nodes and triangle records through one buffer resource (32-bit offsets)
     const __amdgpu_buffer_rsrc_t geo =
         __builtin_amdgcn_make_buffer_rsrc((void*)s.nodes, (short)0, (int)s.geo_bytes, 0x00020000);
@@ -1244,7 +1278,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         // around the step (against `if (busy)`: C2 +3.5 %, trace -4 %)
         {
             const bool done = wf_step<STK, ID, TBL>(s, b, geo, lds, t) & (busy != 0);
-            if (WF_STATS || WF_TIMING) t.nst += busy ? 1 : 0;
+            if (WF_STATS || WF_TIMING || WF_DIAG_COOP) t.nst += busy ? 1 : 0;
             if (WF_STATS && done) atomicAdd(&hist[(t.rid >> 30) * 16 + min(15, 31 - __clz((int)t.nst))], 1u);
             if (WF_TIMING && done) last_ray = (uint64_t)witer << 32 | (t.rid >> 30) << 16 | min(t.nst, 0xffffu);
             if (done) {
@@ -1289,6 +1323,57 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             continue;
         }
         int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
+        // the cooperative finish of lane o's ray (o wave-uniform): its result, or for a
+        // closest-hit ray beyond the finish's limits (-2) a restart by its own lane
+        auto coop_lane = [&](int o) {
+            const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
+            const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
+            auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
+            RayP r;
+            r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
+            r.d = mk3(rdf(t.r.d.x), rdf(t.r.d.y), rdf(t.r.d.z));
+            r.inv = mk3(rdf(t.r.inv.x), rdf(t.r.inv.y), rdf(t.r.inv.z));
+            r.perm = __builtin_amdgcn_readlane(t.r.perm, o);
+            const uint32_t ocur = (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o);
+            const uint32_t olt = (uint32_t)__builtin_amdgcn_readlane(t.lt, o);
+            const uint32_t otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
+            // (closest-hit finishes only in the instantiation that has them: the pipelined
+            // launches' code stays without, C2 -0.9 % with it compiled in)
+            const bool closest = (CC || WF_DIAG_COOP) && orid >= (2u << 30);
+            int res;
+            if (!closest) {
+                res = wf_coop_anyhit<STK>(s, b, geo, lds, fr, r, rdf(t.tMax), ocur, olt, ospa, otl) ? 1 : 0;
+            } else {
+                const int h0 = wf_tri_index<false>(__builtin_amdgcn_readlane(t.hitTri, o));
+                res = wf_coop_closest<STK>(s, geo, lds, fr, b, r, rdf(t.tMax), h0, ocur, olt, ospa, otl);
+            }
+            if (WF_DIAG_COOP && lane == 0) {      // hand-overs (any-hit, closest-hit) and restarts
+                atomicAdd(b.stats + (closest ? 1 : 0), 1ull);
+                if (res == -2) atomicAdd(b.stats + 2, 1ull);
+            }
+            if (WF_DIAG_COOP ? lane == o : busy != 0) {     // (the owner: the wave's one busy lane in product builds)
+                const uint32_t kind = t.rid >> 30;
+                if (res == -2) {         // beyond the cooperative finish's limits: trace it again, alone
+                    wf_ray_start<TBL>(s, t, kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX);
+                    t.rid |= WF_RID_NOCOOP;
+                } else {
+                    const uint32_t p = (uint32_t)PT_CHECK(b.fault, t.rid & WF_RID_P, b.n, PT_SITE_RESULT);
+                    if (kind == 2) b.hit[p] = res;
+                    else b.occ[2 * (size_t)p + kind] = (uint8_t)res;
+                    busy = 0;
+                    t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;
+                }
+            }
+        };
+        if (WF_DIAG_COOP && !TBL && !WF_STATS) {
+            // diagnostic: every ray goes through the cooperative finish once, at its
+            // hash-chosen step (the run loop below stops when one is due)
+            const uint64_t due = __ballot(busy != 0 && wf_coop_due(t));
+            if (due != 0) {
+                coop_lane(__ffsll((long long)due) - 1);
+                continue;
+            }
+        }
         if (WF_COOP_TAIL && !TBL && !WF_STATS) {
             // a wave never steps a lone ray while it could refill around it (back here
             // at one busy lane), and once the queue is exhausted -- the drain -- a
@@ -1298,36 +1383,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
                 const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
                 if (!(orid & WF_RID_NOCOOP) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u &&
-                    ((WF_COOP_TAIL >= 2 && CC) || orid < (2u << 30))) {
-                    auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
-                    RayP r;
-                    r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
-                    r.d = mk3(rdf(t.r.d.x), rdf(t.r.d.y), rdf(t.r.d.z));
-                    r.inv = mk3(rdf(t.r.inv.x), rdf(t.r.inv.y), rdf(t.r.inv.z));
-                    r.perm = __builtin_amdgcn_readlane(t.r.perm, o);
-                    const uint32_t ocur = (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o);
-                    const uint32_t olt = (uint32_t)__builtin_amdgcn_readlane(t.lt, o);
-                    const uint32_t otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
-                    int res;
-                    if (!CC || orid < (2u << 30)) {
-                        res = wf_coop_anyhit<STK>(s, b, geo, lds, r, rdf(t.tMax), ocur, olt, ospa, otl) ? 1 : 0;
-                    } else {
-                        const int h0 = wf_tri_index<false>(__builtin_amdgcn_readlane(t.hitTri, o));
-                        res = wf_coop_closest<STK>(s, geo, lds, b, r, rdf(t.tMax), h0, ocur, olt, ospa, otl);
-                    }
-                    if (busy != 0) {
-                        const uint32_t kind = t.rid >> 30;
-                        if (res == -2) {         // beyond the cooperative finish's capacity: trace it again, alone
-                            wf_ray_start<TBL>(s, t, kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX);
-                            t.rid |= WF_RID_NOCOOP;
-                        } else {
-                            const uint32_t p = (uint32_t)PT_CHECK(b.fault, t.rid & WF_RID_P, b.n, PT_SITE_RESULT);
-                            if (kind == 2) b.hit[p] = res;
-                            else b.occ[2 * (size_t)p + kind] = (uint8_t)res;
-                            busy = 0;
-                            t.lt = 0; t.lc = 0; t.cur = REF_NONE; t.spa &= WF_SPA_STRIDE - 1u;
-                        }
-                    }
+                    ((WF_COOP_TAIL >= 2 && (CC || WF_DIAG_COOP)) || orid < (2u << 30))) {
+                    coop_lane(o);
                     continue;
                 }
                 thr = 0;                 // not for the cooperative finish: step it to the end
@@ -1341,6 +1398,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             for (;;) {
                 step_lane(ident_tag);
                 if (__popcll(__ballot(busy != 0)) <= thr) break;
+                if (WF_DIAG_COOP && !TBL && !WF_STATS && __ballot(busy != 0 && wf_coop_due(t)) != 0) break;
             }
         };
         if (__ballot(busy != 0 && t.r.kz() != 2) == 0) run(std::true_type{});

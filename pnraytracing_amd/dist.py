@@ -32,13 +32,22 @@ class ShardedFrame:
     """Render the rows of this rank and gather the frame to rank 0."""
 
     def __init__(self, tracer, band: int = BAND, device: str | torch.device = "cuda", group=None,
-                 collective: bool = False):
+                 collective: bool = False, shard: tuple[int, int] | None = None):
         self.tracer, self.band, self.group = tracer, band, group
         # collective=True: gather through the process group even with one rank (the
         # RCCL path exercised on a one-GPU box; the image is the same either way)
         self.collective = collective and dist.is_initialized()
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if shard is not None:
+            # (world, rank) of a split rendered WITHOUT a process group: one rank's share
+            # alone (bench.py's PMC pass of rank 0's share); no gather, render() and
+            # pack_rows() use the given split
+            if dist.is_initialized():
+                raise ValueError("ShardedFrame: shard= is for a process without a process group")
+            self.world, self.rank = int(shard[0]), int(shard[1])
+            if not (self.world >= 1 and 0 <= self.rank < self.world):
+                raise ValueError(f"ShardedFrame: bad shard {shard}")
         self.device = torch.device(device)
         H, W = tracer.height, tracer.width
         if H <= 0 or W <= 0:
@@ -93,6 +102,8 @@ class ShardedFrame:
         if self.world == 1 and not self.collective:
             self.image.copy_(self.send)
             return self.image
+        if not dist.is_initialized():
+            raise RuntimeError("ShardedFrame: a shard= split without a process group cannot gather")
         send = self.send.cpu() if self.stage else self.send
         dist.gather(send, self.recv if self.rank == 0 else None, dst=0, group=self.group)
         if self.rank != 0:

@@ -51,6 +51,42 @@ def test_eight_gloo_ranks_gather_equals_one(tmp_path):
     assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
 
 
+def test_bench_self_launch_gloo_two_ranks(tmp_path):
+    """`python3 bench.py --gpus 2 --backend gloo ...` with NO launcher around it
+    (the driver's command shape) starts its own two ranks (VERDICT r4 "Next" 1):
+    the line says n_gpus 2, carries live PMC traffic (rank 0's share, profiled
+    before it joined the group), its own parity check passes, and the gathered
+    image equals the N = 1 image bit for bit."""
+    base = ["--steps", "1", "--warmup", "1", "--config", "C2", "--serial-steps", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    a, b = str(tmp_path / "n1.npy"), str(tmp_path / "n2.npy")
+    subprocess.run([sys.executable, "bench.py", *base, "--no-pmc", "--no-cpu-baseline", "--save-image", a], cwd=REPO,
+                   env=env, check=True, timeout=400, stdout=subprocess.DEVNULL)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", *base, "--save-image", b],
+                       cwd=REPO, env=env, timeout=700, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    import json
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "row-bands8x2"
+    assert d["parity"]["differing"] == 0 and d["parity"]["pixels"] > 0
+    assert d["roofline"]["traffic"] and d["roofline"]["traffic_source"].startswith("live"), d["roofline"]
+    x, y = np.load(a), np.load(b)
+    assert x.shape == y.shape and np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_bench_gpus8_nccl_refused_on_one_gpu():
+    """--gpus 8 over RCCL on this one-GPU box: a non-zero exit and no line, before
+    any rank starts."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "1"], cwd=REPO, env=env,
+                       timeout=120, capture_output=True, text=True)
+    assert r.returncode != 0 and not [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert "needs one GPU per rank" in r.stderr
+
+
 def _single_rank_c4(path):
     from pnraytracing_amd import scenes
     from pnraytracing_amd.tracer import PathTracer

@@ -96,6 +96,17 @@ for name, cfg in cases:
     pt.render(4, 4, 8, 4, 1)                  # a shard as well
     pt.synchronize()                          # raises on any out-of-range index
     print(name, "clean")
+# the bench's own call shape (VERDICT r4 "Next" 3): C2 1920x1080, a 16-frame sizing call,
+# a reset, then four back-to-back 16-frame calls -- 33.2M paths each, staggered over two
+# pipes with the full trace grid and the ev_stage waits -- every index checked
+pt.load(scenes.bunny_c2())
+pt.render(0, 16)
+pt.synchronize()
+pt.reset_accum()
+for k in range(4):
+    pt.render(16 * k, 16)
+pt.synchronize()
+print("C2-1080p-staggered clean")
 if os.environ.get("PNRT_DIAG_FORCE_OOB"):
     try:
         pt.synchronize()
@@ -110,15 +121,16 @@ def test_bounds_checked_variant():
     """variants/libpnrt_bounds.so (-DWF_DIAG_BOUNDS): every fetch / store index of
     the integrator kernels is checked against its array (VERDICT r3 "Next" 5).
     C1, C2, C3 (albedo textures) and C4 at reduced size and a C5-scene frame (4.19M triangles, the wide
-    stack spill area) render with no check tripping; with PNRT_DIAG_FORCE_OOB=1
+    stack spill area) render with no check tripping, and so does the bench's own shape (C2 1080p,
+    sizing call, reset, four staggered 16-frame calls on two pipes); with PNRT_DIAG_FORCE_OOB=1
     one forced out-of-range light-record index is reported (PNRT_E_TRACE naming
     the site) and the child exits non-zero."""
     lib = build.variant_path("bounds")
     assert os.path.exists(lib), "variants/libpnrt_bounds.so not built (__graft_entry__.build())"
     env = dict(os.environ, PNRT_DEVICE_LIB=lib)
     r = subprocess.run([sys.executable, "-c", BOUNDS_CHILD.format(repo=REPO)], env=env, capture_output=True, text=True,
-                       timeout=280)
-    assert r.returncode == 0 and "BOUNDS-CHECK-DONE" in r.stdout, r.stdout + r.stderr[-3000:]
+                       timeout=400)
+    assert r.returncode == 0 and "BOUNDS-CHECK-DONE" in r.stdout and "C2-1080p-staggered clean" in r.stdout, r.stdout + r.stderr[-3000:]
     assert "DIAGNOSTIC BUILD" in r.stdout
     env["PNRT_DIAG_FORCE_OOB"] = "1"
     r = subprocess.run([sys.executable, "-c", BOUNDS_CHILD.format(repo=REPO)], env=env, capture_output=True, text=True,
