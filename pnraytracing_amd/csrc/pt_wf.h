@@ -806,8 +806,8 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 // while the frontier holds at most CAP - 128, else one (depth-first: +1 per
 // descent, at most the tree depth < 63 before a leaf), so it never overflows.
 #ifndef WF_COOP_TAIL
-#define WF_COOP_TAIL 2      // 0 off, 1 any-hit rays, 2 closest-hit rays too (wf_coop_closest) in the
-#endif                      // launches of a call with nothing else in flight (pt_wf_trace<.., CC>, render_batch)
+#define WF_COOP_TAIL 2      // 0 off, 1 any-hit rays, 2 a wave's last rays of any kind together (wf_coop_multi)
+#endif                      // in the launches of a call with nothing else in flight (pt_wf_trace<.., CC>, render_batch)
 // The finishes' limits (pt_diag.h WF_DIAG_COOP_SMALL shrinks them so the fallbacks run):
 // the frontier size above which one entry per iteration is taken (depth-first), the
 // closest-hit candidates the fold takes (at most a wave), the key's sentinel bit
@@ -898,21 +898,27 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
     return hit;
 }
 
-// The same for a closest-hit ray, whose result is the LAST triangle the
+// The same for closest-hit rays, whose result is the LAST triangle the
 // reference's depth-first traversal (near child first, a leaf's triangles in
 // order, :429-461) accepts against a shrinking tMax -- an order-dependent fold,
-// exact only in that order.  Two phases:
+// exact only in that order -- and for a wave's last FEW rays at once, any-hit
+// and closest-hit mixed (wf_coop_multi: up to WF_COOP_MAXRAYS rays, all 64 lanes
+// on one shared frontier).  Two phases:
 // 1. The frontier is walked in any order as above, each entry carrying its
-//    place in the reference's order as a 64-bit key: the rank of the hand-over
-//    entry (pending range 0, node 1, stack top 2, ... bottom), then one bit per
-//    level below it (near child 0, far child 1) ended by a sentinel bit, and the
-//    triangle's place in its leaf in the low 8 bits -- the keys of a subtree lie
-//    between its entry's key and the next one's.  Boxes are culled, and
-//    triangles accepted, against the relaxed bound E (1 + 1e-4), where E is the
-//    least hit distance found so far (from the ray's tMax at the hand-over);
-//    each accepted triangle is a candidate (key, index).
-// 2. The candidates are folded in key order from the hand-over (tMax, hit) with
-//    the exact test and tMax = ts * (1 / det): the reference's result.
+//    ray's index and its place in the reference's order as a 64-bit key: ray
+//    (2 bits), the rank of the hand-over entry (pending range 0, node 1, stack
+//    top 2, ... bottom), then one bit per level below it (near child 0, far child
+//    1) ended by a sentinel bit, and the triangle's place in its leaf in the low
+//    8 bits -- the keys of a subtree lie between its entry's key and the next
+//    one's.  A closest-hit ray's boxes are culled, and its triangles accepted,
+//    against the relaxed bound E (1 + 1e-4), where E is the least hit distance
+//    found for that ray so far (from its tMax at the hand-over; an LDS atomic
+//    min per ray); each accepted triangle is a candidate (key, index).  An any-hit
+//    ray uses its fixed tMax, and its first accepted triangle ends it (its
+//    remaining entries are skipped).
+// 2. Each closest-hit ray's candidates are folded in key order from the
+//    hand-over (tMax, hit) with the exact test and tMax = ts * (1 / det): the
+//    reference's result.
 // Why the candidates suffice: let B be the least distance among the triangles
 // the exact test accepts.  Every triangle within B (1 + 5e-5) of it is a
 // candidate (E >= B, and the 1e-4 margin dwarfs the test's rounding); once the
@@ -920,48 +926,99 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
 // triangle beyond B (1 + 1e-4) again, nor did anything it accepted before change
 // which of them it accepts first (all lie beyond that with margin) -- so both
 // folds accept the same triangles from there on and end on the same one.
-// Fallback: a key deeper than 47 levels below the hand-over, or a frontier plus
-// candidates beyond the capacity, returns -2 and the ray is traced again from
-// its start by its own lane (WF_RID_NOCOOP; rare, exact either way).
+// The frontier: the wave's LDS stack rows 0 .. STK-1 (16-B entries, (ref, z) +
+// key); row STK holds the ray table (64 B per ray: origin, perm; direction,
+// tMax; 1/direction, E; kind, done, hit at the hand-over, result).
+// Fallback: a closest-hit key deeper than 46 levels below the hand-over, or a
+// frontier plus candidates beyond the capacity, returns -2 for every ray; more
+// than WF_COOP_MAXCAND candidates returns -2 for the closest-hit rays.  A -2 ray
+// is traced again from its start by its own lane (WF_RID_NOCOOP; rare, exact
+// either way).  The caller guarantees sum over the rays of (stack depth + 2) <= 64.
+#ifndef WF_COOP_MAXRAYS
+#define WF_COOP_MAXRAYS 4
+#endif
 template <int STK>
-PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const uint2* lds, uint2* fr, const WfBufs& b,
-                           const RayP& r, float tMax0, int hit0, uint32_t cur, uint32_t lt, uint32_t spa, uint32_t otl) {
+PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const uint2* lds, uint2* fr, const WfBufs& b,
+                         const TravState& t, uint64_t owners) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-    constexpr uint32_t CAP = (STK + 1) * 32u;           // 16-B entries: (ref, z) + key
+    constexpr uint32_t NSLOT = STK * 64u;              // the wave's 8-B frontier slots (rows 0 .. STK-1)
+    constexpr uint32_t CAP = NSLOT / 2u;               // 16-B entries
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
-    auto at = [&](uint32_t i) -> char* {                 // the wave's i-th 8-B LDS slot of the frontier area
-        i = (uint32_t)PT_CHECK(b.fault, i, 2u * CAP, PT_SITE_COOP);
+    auto at = [&](uint32_t i) -> char* {                // the wave's i-th 8-B frontier slot
+        i = (uint32_t)PT_CHECK(b.fault, i, NSLOT, PT_SITE_COOP);
         return reinterpret_cast<char*>(fr) + (i >> 6) * WF_SPA_STRIDE + 8u * (wbase + (i & 63u));
     };
     auto put = [&](uint32_t e, uint2 v, uint64_t key) {
         *reinterpret_cast<uint2*>(at(2u * e)) = v;
         *reinterpret_cast<uint2*>(at(2u * e + 1u)) = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
     };
-    const bool cull = r.cull_ok();
-    const uint64_t TOP = 1ull << WF_COOP_KEYTOP;
-    const uint32_t sp = spa >> WF_SPA_SHIFT;
+    // the ray table: row STK of the wave (512 contiguous bytes), 64 B per ray
+    char* const tab = reinterpret_cast<char*>(fr) + STK * WF_SPA_STRIDE + 8u * wbase;
+    auto row = [&](uint32_t r, uint32_t q) -> float4* {
+        return reinterpret_cast<float4*>(tab + ((uint32_t)PT_CHECK(b.fault, r, WF_COOP_MAXRAYS, PT_SITE_COOP) * 64u + q * 16u));
+    };
+    const uint64_t TOP = 1ull << (WF_COOP_KEYTOP - 1);   // (bits 62-63 ray, 55-61 rank)
+    const uint32_t nr = (uint32_t)__popcll(owners);
+    const bool isOwner = ((owners >> lane) & 1ull) != 0;
+    const uint32_t myr = lanes_below(owners);
+    // the owners' rays into the table
+    if (isOwner) {
+        const bool closest = t.rid >= (2u << 30);
+        row(myr, 0)[0] = make_float4(t.r.o.x, t.r.o.y, t.r.o.z, __int_as_float(t.r.perm));
+        row(myr, 1)[0] = make_float4(t.r.d.x, t.r.d.y, t.r.d.z, t.tMax);
+        row(myr, 2)[0] = make_float4(t.r.inv.x, t.r.inv.y, t.r.inv.z, t.tMax);
+        row(myr, 3)[0] = make_float4(__int_as_float(closest ? 1 : 0), __int_as_float(0),
+                                     __int_as_float(wf_tri_index<false>(t.hitTri)), __int_as_float(0));
+    }
+    // the initial frontier: ray r's stack entries, its node to visit and its pending
+    // range, on lanes [base_r, base_r + sp_r + 2)
+    uint32_t o_of[WF_COOP_MAXRAYS], base_of[WF_COOP_MAXRAYS + 1];
+    {
+        uint64_t m = owners;
+        uint32_t base = 0;
+#pragma unroll
+        for (int r = 0; r < WF_COOP_MAXRAYS; ++r) {
+            const int o = m ? __ffsll((long long)m) - 1 : 0;
+            o_of[r] = (uint32_t)o;
+            base_of[r] = base;
+            if (m) base += (((uint32_t)__builtin_amdgcn_readlane((int)t.spa, o)) >> WF_SPA_SHIFT) + 2u;
+            m &= m - 1;
+        }
+        base_of[WF_COOP_MAXRAYS] = 64u;
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 1; q < WF_COOP_MAXRAYS; ++q) r += (q < (int)nr && lane >= base_of[q]) ? 1u : 0u;
+    uint32_t o = o_of[0], jb = base_of[0];
+#pragma unroll
+    for (int q = 1; q < WF_COOP_MAXRAYS; ++q) { o = r == (uint32_t)q ? o_of[q] : o; jb = r == (uint32_t)q ? base_of[q] : jb; }
+    const uint32_t ospa = (uint32_t)__shfl((int)t.spa, (int)o);
+    const uint32_t ocur = (uint32_t)__shfl((int)t.cur, (int)o);
+    const uint32_t olt = (uint32_t)__shfl(t.lt, (int)o);
+    const uint32_t sp = ospa >> WF_SPA_SHIFT, otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
+    const uint32_t j = lane - jb;
     uint2 e = make_uint2(REF_NONE, 0u);
-    uint64_t key = 0;
-    if (lane < sp) {
-        const uint32_t a = lane * WF_SPA_STRIDE + 8u * otl;
-        if (lane < (uint32_t)STK) {
+    uint64_t key = (uint64_t)r << 62;
+    const bool inRange = r < nr && j < sp + 2u;
+    if (inRange && j < sp) {
+        const uint32_t a = j * WF_SPA_STRIDE + 8u * otl;
+        if (j < (uint32_t)STK) {
             e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
         } else {
-            (void)PT_CHECK(b.fault, lane - (uint32_t)STK, b.ovf_stride, PT_SITE_SPILL);
+            (void)PT_CHECK(b.fault, j - (uint32_t)STK, b.ovf_stride, PT_SITE_SPILL);
             const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
             e = make_uint2(v.x, v.y);
         }
-        key = ((uint64_t)(2u + (sp - 1u - lane)) << 56) | TOP;
+        key |= ((uint64_t)(2u + (sp - 1u - j)) << 55) | TOP;
     }
-    if (lane == sp) { e = make_uint2(cur, 0u); key = (1ull << 56) | TOP; }
-    if (lane == sp + 1) { e = make_uint2(lt, 0u); key = TOP; }
-    const bool valid = (lane < sp) | ((lane == sp) & (cur != REF_NONE)) |
-                       ((lane == sp + 1) & (lt >= (REF_LEAF | (1u << 24))));
+    if (inRange && j == sp) { e = make_uint2(ocur, 0u); key |= (1ull << 55) | TOP; }
+    if (inRange && j == sp + 1u) { e = make_uint2(olt, 0u); key |= TOP; }
+    const bool valid = inRange & ((j < sp) | ((j == sp) & (ocur != REF_NONE)) |
+                                  ((j == sp + 1u) & (olt >= (REF_LEAF | (1u << 24)))));
     const uint64_t m0 = __ballot(valid);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the owner's slots are read before any write
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the owners' slots are read before any write
     if (valid) put(lanes_below(m0), e, key);
     uint32_t size = (uint32_t)__popcll(m0), ncand = 0;
-    float E = tMax0;
     bool fail = false;
     while (size > 0) {
         const uint32_t k = size + ncand > WF_COOP_WIDE(CAP) ? 1u : min(size, 64u);
@@ -974,10 +1031,19 @@ PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const 
             fk = ((uint64_t)kk.y << 32) | kk.x;
         }
         size -= k;
-        const float er = E * 1.0001f;                      // the relaxed bound
+        const uint32_t fr_r = (uint32_t)(fk >> 62);
+        // the entry's ray (lanes without an entry read row 0: unused)
+        const float4 T0 = row(fr_r, 0)[0], T1 = row(fr_r, 1)[0], T2 = row(fr_r, 2)[0], T3 = row(fr_r, 3)[0];
+        RayP ry;
+        ry.o = mk3(T0.x, T0.y, T0.z); ry.perm = __float_as_int(T0.w);
+        ry.d = mk3(T1.x, T1.y, T1.z); ry.inv = mk3(T2.x, T2.y, T2.z);
+        const bool closest = __float_as_int(T3.x) != 0, done = __float_as_int(T3.y) != 0;
+        // closest hit: the relaxed bound from E; any hit: the fixed tMax
+        const float er = closest ? T2.w * 1.0001f : T1.w;
         const float tmc = er * 1.000001f;
         const float zc = tmc <= 1e-20f ? 1e-20f : tmc;
-        const bool take = mine & (f.x != REF_NONE) & !(cull & (__uint_as_float(f.y) > zc));
+        const bool cull = ry.cull_ok();
+        const bool take = mine & !done & (f.x != REF_NONE) & !(cull & (__uint_as_float(f.y) > zc));
         const bool isTri = take & (f.x >= (REF_LEAF | (1u << 24)));
         const bool isNode = take & ((f.x & REF_LEAF) == 0u);
         const uint32_t offT = s.geo_tri_off + __umul24(f.x, 48u), offN = isNode ? f.x * 64u : REF_NONE * 64u;
@@ -985,45 +1051,50 @@ PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const 
         const float4 q0 = geo_load(geo, off), q1 = geo_load(geo, off + 16u), q2 = geo_load(geo, off + 32u),
                      q3 = geo_load(geo, offN + 48u);
         float e0, e1, e2, det, ts;
-        const bool acc = tri_test<false>(r, q0, q1, q2, er, e0, e1, e2, det, ts) & isTri;
-        const float th = acc ? ts * (1.0f / det) : er;
-        // E = the least distance found (a non-finite one ends the cooperation)
-        fail |= __ballot(acc & !(pnm_fabs(th) < 3.0e38f)) != 0;
-        float tmin = th;
-        for (int o = 32; o > 0; o >>= 1) tmin = fminf(tmin, __shfl_xor(tmin, o));
-        E = fminf(E, tmin);
+        const bool acc = tri_test<false>(ry, q0, q1, q2, er, e0, e1, e2, det, ts) & isTri;
+        const bool accC = acc & closest;
+        if (acc & !closest) row(fr_r, 3)->y = __int_as_float(1);          // an any-hit ray is occluded
+        if (accC) {
+            const float th = ts * (1.0f / det);
+            // E = the least distance found (a positive float: uint order); a non-finite one ends the cooperation
+            fail |= !(pnm_fabs(th) < 3.0e38f);
+            __hip_atomic_fetch_min(reinterpret_cast<uint32_t*>(&row(fr_r, 2)->w), __float_as_uint(th), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         float zloL, zloR;
-        bool hL = box_fast<false>(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
-        bool hR = box_fast<false>(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
+        bool hL = box_fast<false>(ry, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, zloL);
+        bool hR = box_fast<false>(ry, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, zloR);
         hL = hL & !(cull & (zloL > zc)) & isNode;
         hR = hR & !(cull & (zloR > zc)) & isNode;
         // children and their keys: near child (:448) = key - sent + sent / 2, far = key + sent / 2
-        const uint64_t pk = fk & ~0xffull;
+        const uint64_t pk = fk & ~0xffull & ((1ull << 55) - 1ull);
         const uint64_t sent = pk & (0ull - pk);
-        fail |= __ballot(isNode & (sent <= 0x100ull)) != 0;
-        const bool rightFirst = ((uint32_t)r.perm & __float_as_uint(q3.z)) != 0u;
-        const uint64_t kNear = fk - sent + (sent >> 1), kFar = fk + (sent >> 1);
+        fail |= isNode & closest & (sent <= 0x100ull);     // deeper than a closest-hit key holds
+        const bool rightFirst = ((uint32_t)ry.perm & __float_as_uint(q3.z)) != 0u;
+        // (an any-hit ray's entries keep their key: only its ray index is read, and the
+        // key arithmetic past its depth must not carry into it)
+        const uint64_t kNear = closest ? fk - sent + (sent >> 1) : fk, kFar = closest ? fk + (sent >> 1) : fk;
         const uint32_t rest = f.x + (1u - (1u << 24));           // first + 1, count - 1
         const bool cA = isTri ? (rest >= (REF_LEAF | (1u << 24))) : (hL & (__float_as_uint(q3.x) != REF_LEAF));
         const bool cB = hR & (__float_as_uint(q3.y) != REF_LEAF);
         const uint2 eA = isTri ? make_uint2(rest, 0u) : make_uint2(__float_as_uint(q3.x), __float_as_uint(zloL));
         const uint2 eB = make_uint2(__float_as_uint(q3.y), __float_as_uint(zloR));
-        const uint64_t kA = isTri ? fk + 1u : (rightFirst ? kFar : kNear), kB = rightFirst ? kNear : kFar;
-        const uint64_t bA = __ballot(cA), bB = __ballot(cB), bC = __ballot(acc);
+        const uint64_t kA = isTri ? fk + (closest ? 1u : 0u) : (rightFirst ? kFar : kNear), kB = rightFirst ? kNear : kFar;
+        const uint64_t bA = __ballot(cA), bB = __ballot(cB), bC = __ballot(accC);
         const uint32_t nnew = (uint32_t)(__popcll(bA) + __popcll(bB)), nc = (uint32_t)__popcll(bC);
-        fail |= size + nnew + ncand + nc > CAP;
-        if (fail) break;
+        const bool wfail = (__ballot(fail) != 0) | (size + nnew + ncand + nc > CAP);
+        if (wfail) { fail = true; break; }
         const uint32_t base = size + lanes_below(bA) + lanes_below(bB);
         if (cA) put(base, eA, kA);
         if (cB) put(base + (cA ? 1u : 0u), eB, kB);
         // candidates from the top of the area down: (key, triangle index)
-        if (acc) put(CAP - 1u - ncand - lanes_below(bC), make_uint2(f.x & 0xffffffu, 0u), fk);
+        if (accC) put(CAP - 1u - ncand - lanes_below(bC), make_uint2(f.x & 0xffffffu, 0u), fk);
         size += nnew;
         ncand += nc;
     }
-    if (fail || ncand > WF_COOP_MAXCAND) return -2;
-    // phase 2: the exact fold over the candidates in key (= the reference's) order
-    const bool own = lane < ncand;
+    // phase 2: per closest-hit ray, the exact fold over its candidates in key (= the reference's) order;
+    // the results into the table's last word (-2: restart)
+    const bool own = !fail && lane < ncand && ncand <= WF_COOP_MAXCAND;
     uint32_t tri = 0;
     uint64_t ck = ~0ull;
     if (own) {
@@ -1034,27 +1105,48 @@ PN_DEV int wf_coop_closest(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const 
     }
     const uint32_t toff = own ? s.geo_tri_off + tri * 48u : REF_NONE * 64u;
     const float4 c0 = geo_load(geo, toff), c1 = geo_load(geo, toff + 16u), c2 = geo_load(geo, toff + 32u);
-    float tm = tMax0;
-    int hit = hit0;
-    uint64_t after = 0;               // keys <= after are behind the fold
-    bool first = true;
-    for (uint32_t guard = 0; guard <= ncand; ++guard) {
-        float e0, e1, e2, det, ts;
-        const bool pass = own & (first | (ck > after)) & tri_test<false>(r, c0, c1, c2, tm, e0, e1, e2, det, ts);
-        if (__ballot(pass) == 0) break;
-        uint64_t kmin = pass ? ck : ~0ull;
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t v = ((uint64_t)(uint32_t)__shfl_xor((int)(kmin >> 32), o) << 32) |
-                               (uint32_t)__shfl_xor((int)(uint32_t)kmin, o);
-            kmin = v < kmin ? v : kmin;
+    for (uint32_t q = 0; q < nr; ++q) {
+        const float4 T0 = row(q, 0)[0], T1 = row(q, 1)[0], T2 = row(q, 2)[0], T3 = row(q, 3)[0];
+        const bool closest = __float_as_int(T3.x) != 0;
+        int res;
+        if (fail) {
+            res = -2;
+        } else if (!closest) {
+            res = __float_as_int(T3.y);                   // occluded
+        } else if (ncand > WF_COOP_MAXCAND) {
+            res = -2;
+        } else {
+            RayP ry;
+            ry.o = mk3(T0.x, T0.y, T0.z); ry.perm = __float_as_int(T0.w);
+            ry.d = mk3(T1.x, T1.y, T1.z); ry.inv = mk3(T2.x, T2.y, T2.z);
+            const bool mineq = own & ((uint32_t)(ck >> 62) == q);
+            float tm = T1.w;
+            int hit = __float_as_int(T3.z);
+            uint64_t after = 0;               // keys <= after are behind the fold
+            bool first = true;
+            for (uint32_t guard = 0; guard <= ncand; ++guard) {
+                float e0, e1, e2, det, ts;
+                const bool pass = mineq & (first | (ck > after)) & tri_test<false>(ry, c0, c1, c2, tm, e0, e1, e2, det, ts);
+                if (__ballot(pass) == 0) break;
+                uint64_t kmin = pass ? ck : ~0ull;
+                for (int w = 32; w > 0; w >>= 1) {
+                    const uint64_t v = ((uint64_t)(uint32_t)__shfl_xor((int)(kmin >> 32), w) << 32) |
+                                       (uint32_t)__shfl_xor((int)(uint32_t)kmin, w);
+                    kmin = v < kmin ? v : kmin;
+                }
+                const int jw = __ffsll((long long)__ballot(pass & (ck == kmin))) - 1;
+                tm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts * (1.0f / det)), jw));
+                hit = __builtin_amdgcn_readlane((int)tri, jw);
+                after = kmin;
+                first = false;
+            }
+            res = hit;
         }
-        const int j = __ffsll((long long)__ballot(pass & (ck == kmin))) - 1;
-        tm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts * (1.0f / det)), j));
-        hit = __builtin_amdgcn_readlane((int)tri, j);
-        after = kmin;
-        first = false;
+        if (lane == 0) row(q, 3)->w = __int_as_float(res);
     }
-    return hit;
+    int res = 0;
+    if (isOwner) res = __float_as_int(row(myr, 3)->w);
+    return res;
 }
 
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
@@ -1091,18 +1183,22 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 8      // waves per SIMD (64 VGPRs: no SLP packing, one-register stack position)
 #endif
-// CC: closest-hit rays get the cooperative finish too (wf_coop_closest) -- its own
+// CC: a wave's last rays, closest-hit ones included, get the cooperative finish (wf_coop_multi) -- its own
 // instantiation, launched for a call with nothing else in flight, so the
 // pipelined launches run code without it (C2 -0.9 % with it compiled in)
 // WF_DIAG_COOP builds: the lane steps after which a ray is handed to the cooperative
-// finish, 0..WF_DIAG_COOP, a hash of its kind and path entry
-PN_DEV bool wf_coop_due(const TravState& t) {
-    uint32_t h = (t.rid & ~WF_RID_NOCOOP) * 0x9E3779B1u;
+// finish, 0..WF_DIAG_COOP, a hash of its kind and path entry (and a stack shallow
+// enough for WF_COOP_MAXRAYS rays to share the wave's 64 lanes at the hand-over)
+PN_DEV uint32_t wf_coop_hash(uint32_t rid) {
+    uint32_t h = (rid & ~WF_RID_NOCOOP) * 0x9E3779B1u;
     h ^= h >> 15;
     h *= 0x85EBCA6Bu;
     h ^= h >> 13;
-    return !(t.rid & WF_RID_NOCOOP) && t.nst >= h % (uint32_t)(WF_DIAG_COOP + 1) &&
-           (t.spa >> WF_SPA_SHIFT) + 2u <= 64u;
+    return h;
+}
+PN_DEV bool wf_coop_due(const TravState& t) {
+    return !(t.rid & WF_RID_NOCOOP) && t.nst >= wf_coop_hash(t.rid) % (uint32_t)(WF_DIAG_COOP + 1) &&
+           (t.spa >> WF_SPA_SHIFT) + 2u <= 64u / WF_COOP_MAXRAYS;
 }
 template <int STK, bool TBL, bool CC = false>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
@@ -1323,37 +1419,16 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             continue;
         }
         int thr = (__popcll(busym) * WF_REFILL_PCT) / 100;
-        // the cooperative finish of lane o's ray (o wave-uniform): its result, or for a
-        // closest-hit ray beyond the finish's limits (-2) a restart by its own lane
-        auto coop_lane = [&](int o) {
-            const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
-            const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
-            auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
-            RayP r;
-            r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
-            r.d = mk3(rdf(t.r.d.x), rdf(t.r.d.y), rdf(t.r.d.z));
-            r.inv = mk3(rdf(t.r.inv.x), rdf(t.r.inv.y), rdf(t.r.inv.z));
-            r.perm = __builtin_amdgcn_readlane(t.r.perm, o);
-            const uint32_t ocur = (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o);
-            const uint32_t olt = (uint32_t)__builtin_amdgcn_readlane(t.lt, o);
-            const uint32_t otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
-            // (closest-hit finishes only in the instantiation that has them: the pipelined
-            // launches' code stays without, C2 -0.9 % with it compiled in)
-            const bool closest = (CC || WF_DIAG_COOP) && orid >= (2u << 30);
-            int res;
-            if (!closest) {
-                res = wf_coop_anyhit<STK>(s, b, geo, lds, fr, r, rdf(t.tMax), ocur, olt, ospa, otl) ? 1 : 0;
-            } else {
-                const int h0 = wf_tri_index<false>(__builtin_amdgcn_readlane(t.hitTri, o));
-                res = wf_coop_closest<STK>(s, geo, lds, fr, b, r, rdf(t.tMax), h0, ocur, olt, ospa, otl);
-            }
-            if (WF_DIAG_COOP && lane == 0) {      // hand-overs (any-hit, closest-hit) and restarts
-                atomicAdd(b.stats + (closest ? 1 : 0), 1ull);
+        // the cooperative finishes.  Owner lanes take the result -- or, for -2 (beyond a
+        // finish's limits), restart their ray from the root, traced alone to the end
+        auto coop_result = [&](bool owner, int res) {
+            if (WF_DIAG_COOP && owner) {          // rays handed over (any-hit, closest-hit), restarts
+                atomicAdd(b.stats + (t.rid >= (2u << 30) ? 1 : 0), 1ull);
                 if (res == -2) atomicAdd(b.stats + 2, 1ull);
             }
-            if (WF_DIAG_COOP ? lane == o : busy != 0) {     // (the owner: the wave's one busy lane in product builds)
+            if (owner) {
                 const uint32_t kind = t.rid >> 30;
-                if (res == -2) {         // beyond the cooperative finish's limits: trace it again, alone
+                if (res == -2) {
                     wf_ray_start<TBL>(s, t, kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX);
                     t.rid |= WF_RID_NOCOOP;
                 } else {
@@ -1365,31 +1440,77 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 }
             }
         };
+        // one any-hit ray (lane o, wave-uniform), 8-B frontier entries
+        auto coop_anyhit = [&](int o) {
+            const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
+            auto rdf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), o)); };
+            RayP r;
+            r.o = mk3(rdf(t.r.o.x), rdf(t.r.o.y), rdf(t.r.o.z));
+            r.d = mk3(rdf(t.r.d.x), rdf(t.r.d.y), rdf(t.r.d.z));
+            r.inv = mk3(rdf(t.r.inv.x), rdf(t.r.inv.y), rdf(t.r.inv.z));
+            r.perm = __builtin_amdgcn_readlane(t.r.perm, o);
+            const uint32_t ocur = (uint32_t)__builtin_amdgcn_readlane((int)t.cur, o);
+            const uint32_t olt = (uint32_t)__builtin_amdgcn_readlane(t.lt, o);
+            const uint32_t otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
+            const int res = wf_coop_anyhit<STK>(s, b, geo, lds, fr, r, rdf(t.tMax), ocur, olt, ospa, otl) ? 1 : 0;
+            coop_result(WF_DIAG_COOP ? lane == o : busy != 0, res);   // (the owner: the wave's one busy lane in product builds)
+        };
+        // the rays of lanes `owners` (<= WF_COOP_MAXRAYS, any kinds), one shared frontier
+        constexpr bool MULTI = CC || WF_DIAG_COOP;
+        auto coop_multi = [&](uint64_t owners) {
+            if (WF_DIAG_COOP && lane == 0 && __popcll(owners) > 1) atomicAdd(b.stats + 3, 1ull);
+            const int res = wf_coop_multi<STK>(s, geo, lds, fr, b, t, owners);
+            coop_result(((owners >> lane) & 1ull) != 0, res);
+        };
         if (WF_DIAG_COOP && !TBL && !WF_STATS) {
-            // diagnostic: every ray goes through the cooperative finish once, at its
-            // hash-chosen step (the run loop below stops when one is due)
-            const uint64_t due = __ballot(busy != 0 && wf_coop_due(t));
+            // diagnostic: every ray goes through a cooperative finish once, at its
+            // hash-chosen step (the run loop below stops when one is due): up to
+            // WF_COOP_MAXRAYS due rays together, or a lone any-hit ray alone (by hash)
+            uint64_t due = __ballot(busy != 0 && wf_coop_due(t));
             if (due != 0) {
-                coop_lane(__ffsll((long long)due) - 1);
+                uint64_t own = 0;
+                for (int q = 0; q < WF_COOP_MAXRAYS && due; ++q) { own |= due & (0ull - due); due &= due - 1; }
+                const int o = __ffsll((long long)own) - 1;
+                const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
+                if (__popcll(own) == 1 && orid < (2u << 30) && (wf_coop_hash(orid) & 1u)) coop_anyhit(o);
+                else coop_multi(own);
                 continue;
             }
         }
         if (WF_COOP_TAIL && !TBL && !WF_STATS) {
-            // a wave never steps a lone ray while it could refill around it (back here
-            // at one busy lane), and once the queue is exhausted -- the drain -- a
-            // wave down to one ray finishes it with all its lanes
-            if (__popcll(busym) == 1 && exhausted) {
-                const int o = __ffsll((long long)busym) - 1;
-                const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
-                const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
-                if (!(orid & WF_RID_NOCOOP) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u &&
-                    ((WF_COOP_TAIL >= 2 && (CC || WF_DIAG_COOP)) || orid < (2u << 30))) {
-                    coop_lane(o);
-                    continue;
+            const int nb = __popcll(busym);
+            if (MULTI && WF_COOP_TAIL >= 2) {
+                // lone calls: once the queue is exhausted -- the drain -- a wave down to
+                // WF_COOP_MAXRAYS rays finishes them with all its lanes together
+                if (exhausted && nb <= WF_COOP_MAXRAYS) {
+                    bool ok = __ballot(busy != 0 && (t.rid & WF_RID_NOCOOP) != 0) == 0;
+                    uint32_t need = 0;
+                    for (uint64_t m = busym; m; m &= m - 1)
+                        need += ((uint32_t)__builtin_amdgcn_readlane((int)t.spa, __ffsll((long long)m) - 1) >> WF_SPA_SHIFT) + 2u;
+                    if (ok && need <= 64u) {
+                        coop_multi(busym);
+                        continue;
+                    }
+                    thr = nb - 1;        // step until one of them is done, then look again
+                } else {
+                    thr = exhausted ? max(thr, WF_COOP_MAXRAYS) : (nb == 1 ? 0 : max(thr, 1));
                 }
-                thr = 0;                 // not for the cooperative finish: step it to the end
             } else {
-                thr = __popcll(busym) == 1 ? 0 : max(thr, 1);   // come back here when one ray is left
+                // pipelined launches: a wave never steps a lone ray while it could refill
+                // around it (back here at one busy lane), and once the queue is exhausted
+                // a wave down to one any-hit ray finishes it with all its lanes
+                if (nb == 1 && exhausted) {
+                    const int o = __ffsll((long long)busym) - 1;
+                    const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
+                    const uint32_t ospa = (uint32_t)__builtin_amdgcn_readlane((int)t.spa, o);
+                    if (!(orid & WF_RID_NOCOOP) && (ospa >> WF_SPA_SHIFT) + 2u <= 64u && orid < (2u << 30)) {
+                        coop_anyhit(o);
+                        continue;
+                    }
+                    thr = 0;             // not for the cooperative finish: step it to the end
+                } else {
+                    thr = nb == 1 ? 0 : max(thr, 1);   // come back here when one ray is left
+                }
             }
         }
         // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------

@@ -9,7 +9,10 @@ env shadow rays (any-hit) and continuation rays (closest-hit), in every
 launch -- to the finish after a hash-chosen 0..24 lane steps, with every
 fetch / store / frontier index bounds-checked:
 
-* ``coop``       the product limits: the finish completes nearly every ray;
+* ``coop``       the product limits: the finish completes nearly every ray --
+                 up to four due rays of a wave on one shared frontier
+                 (wf_coop_multi, the lone calls' drain finish), a lone any-hit
+                 ray on its own (wf_coop_anyhit, the pipelined launches');
 * ``coopsmall``  the limits shrunk (one-entry depth-first regime above 8
                  frontier entries, at most 2 candidates, keys 12 levels deep):
                  closest-hit rays routinely come back as -2 and are traced
@@ -42,9 +45,9 @@ def _run(lib, which, *extra, timeout=400):
     r = subprocess.run([sys.executable, os.path.join(HERE, "coop_worker.py"), which, *extra], env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0 and "COOP-WORKER-DONE" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
-    tot = [0, 0, 0]
-    for m in re.finditer(r"\[coop\] bounce \d+ n=\d+ anyhit=(\d+) closest=(\d+) restarts=(\d+)", r.stderr):
-        for k in range(3):
+    tot = [0, 0, 0, 0]
+    for m in re.finditer(r"\[coop\] bounce \d+ n=\d+ anyhit=(\d+) closest=(\d+) restarts=(\d+) multi=(\d+)", r.stderr):
+        for k in range(4):
             tot[k] += int(m.group(k + 1))
     return r.stdout, tot
 
@@ -53,18 +56,20 @@ def _run(lib, which, *extra, timeout=400):
 def test_forced_cooperative_finish_fixed_scenes(variant):
     lib = build.variant_path(variant)
     assert os.path.exists(lib), f"variants/libpnrt_{variant}.so not built (__graft_entry__.build())"
-    out, (anyhit, closest, restarts) = _run(lib, "fixed")
+    out, (anyhit, closest, restarts, multi) = _run(lib, "fixed")
     assert "DIAGNOSTIC BUILD" in out
-    print(f"{variant}: hand-overs any-hit {anyhit}, closest-hit {closest}, restarts {restarts}")
-    assert anyhit > 1000 and closest > 1000
+    print(f"{variant}: rays handed over any-hit {anyhit}, closest-hit {closest}, restarts {restarts}, "
+          f"finishes of 2-4 rays together {multi}")
+    assert anyhit > 1000 and closest > 1000 and multi > 100
     assert restarts > (1000 if variant == "coopsmall" else 0)   # (coop: the 65 / 100-triangle leaves)
 
 
 @pytest.mark.parametrize("variant", ["coop", "coopsmall"])
 def test_forced_cooperative_finish_fuzz(variant):
     lib = build.variant_path(variant)
-    out, (anyhit, closest, restarts) = _run(lib, "fuzz")
-    print(f"{variant} fuzz: hand-overs any-hit {anyhit}, closest-hit {closest}, restarts {restarts}")
+    out, (anyhit, closest, restarts, multi) = _run(lib, "fuzz")
+    print(f"{variant} fuzz: rays handed over any-hit {anyhit}, closest-hit {closest}, restarts {restarts}, "
+          f"finishes of 2-4 rays together {multi}")
     assert anyhit > 0 and closest > 0
     if variant == "coopsmall":
         assert restarts > 0

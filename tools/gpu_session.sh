@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box session of round 4, steps chosen by STEPS (space-separated, in order):
+# One GPU-box session (rounds 4-5), steps chosen by STEPS (space-separated, in order):
 #   smoke    __graft_entry__.smoke()
 #   tests    the whole -m gpu suite (TESTS= to narrow it, e.g. TESTS="tests/test_gpu_parity.py")
 #   bench    bench.py C2 default (live PMC, CPU leg with the parity check)   [CONFIGS= for others]
@@ -11,6 +11,8 @@
 #   record   profiles/pmc.json from this session's N = 1 bench lines
 #   shard    the multi-GPU share simulation (per-rank rates at N = 1/2/4/8 on one GPU)
 #   tail     WF_TIMING drain census of the lone-frame (D2) trace launches
+#   coopv    the cooperative-finish tests, verbose (hand-over / restart counts)
+#   abd      A/B of prebuilt variants on D2 / D3 synchronised per frame, no HIP events (VARIANTS, ROUNDS)
 #   fuzz     the widened fuzz campaign (SEEDS=40000 random scenes x 3 kernel modes vs the oracle)
 # Output under gpurun_out/$TAG.  Every GPU step has its own time limit; the first failing
 # step ends the session (no retries).
@@ -78,6 +80,23 @@ for s in ${STEPS:-smoke tests bench}; do
         step $c-kt timeout -k 10 200 python bench.py --config $c --sync-per-frame --steps 240 --warmup 16 --no-cpu-baseline \
           --no-pmc --serial-steps 0 --kernel-times > $O/${c}--sync-per-frame-kernel-times.json 2> $O/${c}-kt.err
         summ $O/${c}--sync-per-frame-kernel-times.json
+      done ;;
+    coopv)     # the cooperative-finish tests verbose: the hand-over / restart counts of the diagnostic libraries
+      step coop-tests timeout -k 10 900 python -u -m pytest tests/test_gpu_coop.py -m gpu -x -v -s --timeout 400 \
+        --timeout-method thread > $O/coop_tests.log 2>&1
+      grep -E "rays handed over|passed|failed" $O/coop_tests.log | tail -8 ;;
+    abd)       # A/B of the reference's dispatch shape (D2 / D3: 512x512, one 1-spp frame per call), synchronised
+               # per frame, no HIP events; VARIANTS as for ab
+      for r in $(seq 1 ${ROUNDS:-2}); do
+        for v in ${VARIANTS}; do
+          lib=""; [ $v != base ] && lib=pnraytracing_amd/variants/libpnrt_$v.so
+          for c in ${AB_DCONFIGS:-D2 D3}; do
+            step abd-$v-$c-$r env PNRT_DEVICE_LIB=$lib timeout -k 10 200 python bench.py --config $c --sync-per-frame \
+              --steps 240 --warmup 16 --no-parity --no-pmc --no-cpu-baseline --serial-steps 0 --no-kernel-events \
+              > $O/abd_${v}_${c}_$r.json 2> $O/abd_${v}_${c}_$r.err
+            summ $O/abd_${v}_${c}_$r.json
+          done
+        done
       done ;;
     ab)
       for r in $(seq 1 ${ROUNDS:-2}); do
