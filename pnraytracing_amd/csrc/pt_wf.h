@@ -722,7 +722,7 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
         t.lt += isTri ? 1 : 0;
         t.lc -= isTri ? 1 : 0;
     } else {
-        t.lt += isTri ? (int)(1u - (1u << 24)) : 0;     // first + 1, count - 1
+        t.lt = isTri ? (int)((uint32_t)t.lt + (1u - (1u << 24))) : t.lt;     // first + 1, count - 1
     }
     // node visit: both child boxes (:447-457), z-slab culling
     const uint4 m = make_uint4(__float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z),
@@ -814,11 +814,9 @@ PN_DEV __attribute__((always_inline)) bool wf_step(const DevScene& s, const WfBu
 #if WF_DIAG_COOP_SMALL
 #define WF_COOP_WIDE(cap) 8u
 #define WF_COOP_MAXCAND 2u
-#define WF_COOP_KEYTOP 20
 #else
 #define WF_COOP_WIDE(cap) ((cap) - 128u)
 #define WF_COOP_MAXCAND 64u
-#define WF_COOP_KEYTOP 55
 #endif
 // The owner's stack lives in `lds` (its slots, depth d at d * stride + 8 * otl, and the
 // spill area); the frontier is built in the wave's slots of `fr` -- the same area as
@@ -906,7 +904,7 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
 // on one shared frontier).  Two phases:
 // 1. The frontier is walked in any order as above, each entry carrying its
 //    ray's index and its place in the reference's order as a 64-bit key: ray
-//    (2 bits), the rank of the hand-over entry (pending range 0, node 1, stack
+//    (2 or 3 bits), the rank of the hand-over entry (pending range 0, node 1, stack
 //    top 2, ... bottom), then one bit per level below it (near child 0, far child
 //    1) ended by a sentinel bit, and the triangle's place in its leaf in the low
 //    8 bits -- the keys of a subtree lie between its entry's key and the next
@@ -929,14 +927,20 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
 // The frontier: the wave's LDS stack rows 0 .. STK-1 (16-B entries, (ref, z) +
 // key); row STK holds the ray table (64 B per ray: origin, perm; direction,
 // tMax; 1/direction, E; kind, done, hit at the hand-over, result).
-// Fallback: a closest-hit key deeper than 46 levels below the hand-over, or a
+// Fallback: a closest-hit key deeper than 45-46 levels below the hand-over, or a
 // frontier plus candidates beyond the capacity, returns -2 for every ray; more
 // than WF_COOP_MAXCAND candidates returns -2 for the closest-hit rays.  A -2 ray
 // is traced again from its start by its own lane (WF_RID_NOCOOP; rare, exact
 // either way).  The caller guarantees sum over the rays of (stack depth + 2) <= 64.
 #ifndef WF_COOP_MAXRAYS
-#define WF_COOP_MAXRAYS 4
+#define WF_COOP_MAXRAYS 4   // rays finished together (<= 8: the ray table fills row STK, 64 B per ray)
 #endif
+#ifndef WF_COOP_ALL
+#define WF_COOP_ALL 0       // 1: pipelined launches finish their drain the same way (A/B switch)
+#endif
+#define WF_COOP_RAYBITS (WF_COOP_MAXRAYS > 4 ? 3 : 2)      // key bits 63.. : the ray
+#define WF_COOP_RANKSHIFT (64 - WF_COOP_RAYBITS - 7)       // 7 bits below them: the hand-over rank
+static_assert(WF_COOP_MAXRAYS >= 1 && WF_COOP_MAXRAYS <= 8, "the ray table holds at most 8 rays");
 template <int STK>
 PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const uint2* lds, uint2* fr, const WfBufs& b,
                          const TravState& t, uint64_t owners) {
@@ -957,7 +961,9 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
     auto row = [&](uint32_t r, uint32_t q) -> float4* {
         return reinterpret_cast<float4*>(tab + ((uint32_t)PT_CHECK(b.fault, r, WF_COOP_MAXRAYS, PT_SITE_COOP) * 64u + q * 16u));
     };
-    const uint64_t TOP = 1ull << (WF_COOP_KEYTOP - 1);   // (bits 62-63 ray, 55-61 rank)
+    // the key's sentinel bit below the ray and rank fields (the diagnostic small limits: bit 19)
+    const uint64_t TOP = 1ull << (WF_DIAG_COOP_SMALL ? 19 : WF_COOP_RANKSHIFT - 1);
+    constexpr int RS = 64 - WF_COOP_RAYBITS;
     const uint32_t nr = (uint32_t)__popcll(owners);
     const bool isOwner = ((owners >> lane) & 1ull) != 0;
     const uint32_t myr = lanes_below(owners);
@@ -998,7 +1004,7 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
     const uint32_t sp = ospa >> WF_SPA_SHIFT, otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
     const uint32_t j = lane - jb;
     uint2 e = make_uint2(REF_NONE, 0u);
-    uint64_t key = (uint64_t)r << 62;
+    uint64_t key = (uint64_t)r << RS;
     const bool inRange = r < nr && j < sp + 2u;
     if (inRange && j < sp) {
         const uint32_t a = j * WF_SPA_STRIDE + 8u * otl;
@@ -1009,9 +1015,9 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
             const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
             e = make_uint2(v.x, v.y);
         }
-        key |= ((uint64_t)(2u + (sp - 1u - j)) << 55) | TOP;
+        key |= ((uint64_t)(2u + (sp - 1u - j)) << WF_COOP_RANKSHIFT) | TOP;
     }
-    if (inRange && j == sp) { e = make_uint2(ocur, 0u); key |= (1ull << 55) | TOP; }
+    if (inRange && j == sp) { e = make_uint2(ocur, 0u); key |= (1ull << WF_COOP_RANKSHIFT) | TOP; }
     if (inRange && j == sp + 1u) { e = make_uint2(olt, 0u); key |= TOP; }
     const bool valid = inRange & ((j < sp) | ((j == sp) & (ocur != REF_NONE)) |
                                   ((j == sp + 1u) & (olt >= (REF_LEAF | (1u << 24)))));
@@ -1031,7 +1037,7 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
             fk = ((uint64_t)kk.y << 32) | kk.x;
         }
         size -= k;
-        const uint32_t fr_r = (uint32_t)(fk >> 62);
+        const uint32_t fr_r = (uint32_t)(fk >> RS);
         // the entry's ray (lanes without an entry read row 0: unused)
         const float4 T0 = row(fr_r, 0)[0], T1 = row(fr_r, 1)[0], T2 = row(fr_r, 2)[0], T3 = row(fr_r, 3)[0];
         RayP ry;
@@ -1067,7 +1073,7 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
         hL = hL & !(cull & (zloL > zc)) & isNode;
         hR = hR & !(cull & (zloR > zc)) & isNode;
         // children and their keys: near child (:448) = key - sent + sent / 2, far = key + sent / 2
-        const uint64_t pk = fk & ~0xffull & ((1ull << 55) - 1ull);
+        const uint64_t pk = fk & ~0xffull & ((1ull << WF_COOP_RANKSHIFT) - 1ull);
         const uint64_t sent = pk & (0ull - pk);
         fail |= isNode & closest & (sent <= 0x100ull);     // deeper than a closest-hit key holds
         const bool rightFirst = ((uint32_t)ry.perm & __float_as_uint(q3.z)) != 0u;
@@ -1119,7 +1125,7 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
             RayP ry;
             ry.o = mk3(T0.x, T0.y, T0.z); ry.perm = __float_as_int(T0.w);
             ry.d = mk3(T1.x, T1.y, T1.z); ry.inv = mk3(T2.x, T2.y, T2.z);
-            const bool mineq = own & ((uint32_t)(ck >> 62) == q);
+            const bool mineq = own & ((uint32_t)(ck >> RS) == q);
             float tm = T1.w;
             int hit = __float_as_int(T3.z);
             uint64_t after = 0;               // keys <= after are behind the fold
@@ -1456,7 +1462,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             coop_result(WF_DIAG_COOP ? lane == o : busy != 0, res);   // (the owner: the wave's one busy lane in product builds)
         };
         // the rays of lanes `owners` (<= WF_COOP_MAXRAYS, any kinds), one shared frontier
-        constexpr bool MULTI = CC || WF_DIAG_COOP;
+        constexpr bool MULTI = CC || WF_DIAG_COOP || WF_COOP_ALL;
         auto coop_multi = [&](uint64_t owners) {
             if (WF_DIAG_COOP && lane == 0 && __popcll(owners) > 1) atomicAdd(b.stats + 3, 1ull);
             const int res = wf_coop_multi<STK>(s, geo, lds, fr, b, t, owners);
