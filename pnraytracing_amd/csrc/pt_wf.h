@@ -933,8 +933,8 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
 // is traced again from its start by its own lane (WF_RID_NOCOOP; rare, exact
 // either way).  The caller guarantees sum over the rays of (stack depth + 2) <= 64.
 #ifndef WF_COOP_MAXRAYS
-#define WF_COOP_MAXRAYS 4   // rays finished together (<= 8: the ray table fills row STK, 64 B per ray)
-#endif
+#define WF_COOP_MAXRAYS 8   // rays finished together (<= 8: the ray table fills row STK, 64 B per ray;
+#endif                      // D2 synchronised: 2 / 4 / 6 / 8 rays 0.654 / 0.625 / 0.611 / 0.605 ms per frame)
 #ifndef WF_COOP_ALL
 #define WF_COOP_ALL 0       // 1: pipelined launches finish their drain the same way (A/B switch)
 #endif
@@ -977,8 +977,11 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
                                      __int_as_float(wf_tri_index<false>(t.hitTri)), __int_as_float(0));
     }
     // the initial frontier: ray r's stack entries, its node to visit and its pending
-    // range, on lanes [base_r, base_r + sp_r + 2)
-    uint32_t o_of[WF_COOP_MAXRAYS], base_of[WF_COOP_MAXRAYS + 1];
+    // range, items [base_r, base_r + sp_r + 2) of at most 64 -- item l read by lane l,
+    // every read before any write (the owners' stack slots lie in the rows the frontier
+    // overwrites).  (Two items per lane, up to 128: the added registers spilled in the
+    // lone-call kernel's step loop.)
+    uint32_t o_of[WF_COOP_MAXRAYS], base_of[WF_COOP_MAXRAYS];
     {
         uint64_t m = owners;
         uint32_t base = 0;
@@ -986,44 +989,48 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
         for (int r = 0; r < WF_COOP_MAXRAYS; ++r) {
             const int o = m ? __ffsll((long long)m) - 1 : 0;
             o_of[r] = (uint32_t)o;
-            base_of[r] = base;
+            base_of[r] = m ? base : 64u;
             if (m) base += (((uint32_t)__builtin_amdgcn_readlane((int)t.spa, o)) >> WF_SPA_SHIFT) + 2u;
             m &= m - 1;
         }
-        base_of[WF_COOP_MAXRAYS] = 64u;
     }
-    uint32_t r = 0;
+    auto item = [&](uint32_t l, uint2& e, uint64_t& key) -> bool {
+        uint32_t r = 0, o = o_of[0], jb = base_of[0];
 #pragma unroll
-    for (int q = 1; q < WF_COOP_MAXRAYS; ++q) r += (q < (int)nr && lane >= base_of[q]) ? 1u : 0u;
-    uint32_t o = o_of[0], jb = base_of[0];
-#pragma unroll
-    for (int q = 1; q < WF_COOP_MAXRAYS; ++q) { o = r == (uint32_t)q ? o_of[q] : o; jb = r == (uint32_t)q ? base_of[q] : jb; }
-    const uint32_t ospa = (uint32_t)__shfl((int)t.spa, (int)o);
-    const uint32_t ocur = (uint32_t)__shfl((int)t.cur, (int)o);
-    const uint32_t olt = (uint32_t)__shfl(t.lt, (int)o);
-    const uint32_t sp = ospa >> WF_SPA_SHIFT, otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
-    const uint32_t j = lane - jb;
-    uint2 e = make_uint2(REF_NONE, 0u);
-    uint64_t key = (uint64_t)r << RS;
-    const bool inRange = r < nr && j < sp + 2u;
-    if (inRange && j < sp) {
-        const uint32_t a = j * WF_SPA_STRIDE + 8u * otl;
-        if (j < (uint32_t)STK) {
-            e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
-        } else {
-            (void)PT_CHECK(b.fault, j - (uint32_t)STK, b.ovf_stride, PT_SITE_SPILL);
-            const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
-            e = make_uint2(v.x, v.y);
+        for (int q = 1; q < WF_COOP_MAXRAYS; ++q) {
+            const bool in = l >= base_of[q];
+            r = in ? (uint32_t)q : r; o = in ? o_of[q] : o; jb = in ? base_of[q] : jb;
         }
-        key |= ((uint64_t)(2u + (sp - 1u - j)) << WF_COOP_RANKSHIFT) | TOP;
-    }
-    if (inRange && j == sp) { e = make_uint2(ocur, 0u); key |= (1ull << WF_COOP_RANKSHIFT) | TOP; }
-    if (inRange && j == sp + 1u) { e = make_uint2(olt, 0u); key |= TOP; }
-    const bool valid = inRange & ((j < sp) | ((j == sp) & (ocur != REF_NONE)) |
-                                  ((j == sp + 1u) & (olt >= (REF_LEAF | (1u << 24)))));
-    const uint64_t m0 = __ballot(valid);
+        const uint32_t ospa = (uint32_t)__shfl((int)t.spa, (int)o);
+        const uint32_t ocur = (uint32_t)__shfl((int)t.cur, (int)o);
+        const uint32_t olt = (uint32_t)__shfl(t.lt, (int)o);
+        const uint32_t sp = ospa >> WF_SPA_SHIFT, otl = (ospa & (WF_SPA_STRIDE - 1u)) >> 3;
+        const uint32_t j = l - jb;
+        e = make_uint2(REF_NONE, 0u);
+        key = (uint64_t)r << RS;
+        const bool inRange = l >= base_of[0] && j < sp + 2u;
+        if (inRange && j < sp) {
+            const uint32_t a = j * WF_SPA_STRIDE + 8u * otl;
+            if (j < (uint32_t)STK) {
+                e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(lds) + a);
+            } else {
+                (void)PT_CHECK(b.fault, j - (uint32_t)STK, b.ovf_stride, PT_SITE_SPILL);
+                const u2 v = __builtin_amdgcn_raw_buffer_load_b64(wf_ovf_rsrc(b, STK), (int)a, wf_ovf_soff(b), 0);
+                e = make_uint2(v.x, v.y);
+            }
+            key |= ((uint64_t)(2u + (sp - 1u - j)) << WF_COOP_RANKSHIFT) | TOP;
+        }
+        if (inRange && j == sp) { e = make_uint2(ocur, 0u); key |= (1ull << WF_COOP_RANKSHIFT) | TOP; }
+        if (inRange && j == sp + 1u) { e = make_uint2(olt, 0u); key |= TOP; }
+        return inRange & ((j < sp) | ((j == sp) & (ocur != REF_NONE)) |
+                          ((j == sp + 1u) & (olt >= (REF_LEAF | (1u << 24)))));
+    };
+    uint2 e0;
+    uint64_t key0;
+    const bool v0 = item(lane, e0, key0);
+    const uint64_t m0 = __ballot(v0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the owners' slots are read before any write
-    if (valid) put(lanes_below(m0), e, key);
+    if (v0) put(lanes_below(m0), e0, key0);
     uint32_t size = (uint32_t)__popcll(m0), ncand = 0;
     bool fail = false;
     while (size > 0) {
