@@ -10,7 +10,7 @@ launch -- to the finish after a hash-chosen 0..24 lane steps, with every
 fetch / store / frontier index bounds-checked:
 
 * ``coop``       the product limits: the finish completes nearly every ray --
-                 up to four due rays of a wave on one shared frontier
+                 up to eight due rays of a wave on one shared frontier
                  (wf_coop_multi, the lone calls' drain finish), a lone any-hit
                  ray on its own (wf_coop_anyhit, the pipelined launches');
 * ``coopsmall``  the limits shrunk (one-entry depth-first regime above 8
@@ -59,7 +59,7 @@ def test_forced_cooperative_finish_fixed_scenes(variant):
     out, (anyhit, closest, restarts, multi) = _run(lib, "fixed")
     assert "DIAGNOSTIC BUILD" in out
     print(f"{variant}: rays handed over any-hit {anyhit}, closest-hit {closest}, restarts {restarts}, "
-          f"finishes of 2-4 rays together {multi}")
+          f"finishes of 2-8 rays together {multi}")
     assert anyhit > 1000 and closest > 1000 and multi > 100
     assert restarts > (1000 if variant == "coopsmall" else 0)   # (coop: the 65 / 100-triangle leaves)
 
@@ -69,7 +69,7 @@ def test_forced_cooperative_finish_fuzz(variant):
     lib = build.variant_path(variant)
     out, (anyhit, closest, restarts, multi) = _run(lib, "fuzz")
     print(f"{variant} fuzz: rays handed over any-hit {anyhit}, closest-hit {closest}, restarts {restarts}, "
-          f"finishes of 2-4 rays together {multi}")
+          f"finishes of 2-8 rays together {multi}")
     assert anyhit > 0 and closest > 0
     if variant == "coopsmall":
         assert restarts > 0
