@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Record an N = 1 bench line's live-PMC roofline traffic in profiles/pmc.json,
 keyed by config / kernel and the device-source hash, so that a multi-GPU bench
-run (which takes no PMC passes of its own) can report its rank's traffic per
-launch as a labelled derivation (bench.py: the figure x the rank's share of the
+run whose rank-0 PMC passes fail (or run with --no-pmc) can still report its
+rank's traffic per launch as a labelled derivation (bench.py: the figure x the rank's share of the
 rows x its frames per launch / the recorded launch's).
 
     python tools/record_pmc.py BENCH_LINE.json [...]
