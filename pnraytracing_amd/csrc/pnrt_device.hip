@@ -394,11 +394,11 @@ static int report_trace_diag(pnrt_ctx* c, const WfBufs& b, hipStream_t st, int b
         fprintf(stderr, "\n");
     }
     if (WF_DIAG_COOP) {   // cooperative-finish hand-overs of the launch (tests/test_gpu_coop.py)
-        unsigned long long cc[4];
+        unsigned long long cc[5];
         HIPCHK(c, hipStreamSynchronize(st));
         HIPCHK(c, hipMemcpy(cc, b.stats, sizeof cc, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[coop] bounce %d n=%u anyhit=%llu closest=%llu restarts=%llu multi=%llu\n", bounce, b.n, cc[0], cc[1],
-                cc[2], cc[3]);
+        fprintf(stderr, "[coop] bounce %d n=%u anyhit=%llu closest=%llu restarts=%llu multi=%llu deep=%llu\n", bounce, b.n,
+                cc[0], cc[1], cc[2], cc[3], cc[4]);
     }
     if (WF_STATS) {
         unsigned long long stt[8 + 48];

@@ -1200,8 +1200,7 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 // instantiation, launched for a call with nothing else in flight, so the
 // pipelined launches run code without it (C2 -0.9 % with it compiled in)
 // WF_DIAG_COOP builds: the lane steps after which a ray is handed to the cooperative
-// finish, 0..WF_DIAG_COOP, a hash of its kind and path entry (and a stack shallow
-// enough for WF_COOP_MAXRAYS rays to share the wave's 64 lanes at the hand-over)
+// finish, 0..WF_DIAG_COOP, a hash of its kind and path entry
 PN_DEV uint32_t wf_coop_hash(uint32_t rid) {
     uint32_t h = (rid & ~WF_RID_NOCOOP) * 0x9E3779B1u;
     h ^= h >> 15;
@@ -1211,7 +1210,7 @@ PN_DEV uint32_t wf_coop_hash(uint32_t rid) {
 }
 PN_DEV bool wf_coop_due(const TravState& t) {
     return !(t.rid & WF_RID_NOCOOP) && t.nst >= wf_coop_hash(t.rid) % (uint32_t)(WF_DIAG_COOP + 1) &&
-           (t.spa >> WF_SPA_SHIFT) + 2u <= 64u / WF_COOP_MAXRAYS;
+           (t.spa >> WF_SPA_SHIFT) + 2u <= 64u;
 }
 template <int STK, bool TBL, bool CC = false>
 __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
@@ -1472,6 +1471,8 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         constexpr bool MULTI = CC || WF_DIAG_COOP || WF_COOP_ALL;
         auto coop_multi = [&](uint64_t owners) {
             if (WF_DIAG_COOP && lane == 0 && __popcll(owners) > 1) atomicAdd(b.stats + 3, 1ull);
+            if (WF_DIAG_COOP && ((owners >> lane) & 1ull) && (t.spa >> WF_SPA_SHIFT) > (uint32_t)STK)
+                atomicAdd(b.stats + 4, 1ull);       // rays handed over with stack entries in the spill area
             const int res = wf_coop_multi<STK>(s, geo, lds, fr, b, t, owners);
             coop_result(((owners >> lane) & 1ull) != 0, res);
         };
@@ -1481,8 +1482,19 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             // WF_COOP_MAXRAYS due rays together, or a lone any-hit ray alone (by hash)
             uint64_t due = __ballot(busy != 0 && wf_coop_due(t));
             if (due != 0) {
+                // (greedily, while the rays' stack entries fit the 64 initial items: deep
+                // stacks -- entries in the spill area -- are handed over too)
                 uint64_t own = 0;
-                for (int q = 0; q < WF_COOP_MAXRAYS && due; ++q) { own |= due & (0ull - due); due &= due - 1; }
+                uint32_t need = 0;
+                for (int q = 0; q < WF_COOP_MAXRAYS && due; ++q) {
+                    const uint64_t bit = due & (0ull - due);
+                    const uint32_t n = ((uint32_t)__builtin_amdgcn_readlane((int)t.spa, __ffsll((long long)bit) - 1) >>
+                                        WF_SPA_SHIFT) + 2u;
+                    due &= due - 1;
+                    if (need + n > 64u) continue;
+                    need += n;
+                    own |= bit;
+                }
                 const int o = __ffsll((long long)own) - 1;
                 const uint32_t orid = (uint32_t)__builtin_amdgcn_readlane((int)t.rid, o);
                 if (__popcll(own) == 1 && orid < (2u << 30) && (wf_coop_hash(orid) & 1u)) coop_anyhit(o);

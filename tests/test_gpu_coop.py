@@ -45,9 +45,10 @@ def _run(lib, which, *extra, timeout=400):
     r = subprocess.run([sys.executable, os.path.join(HERE, "coop_worker.py"), which, *extra], env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0 and "COOP-WORKER-DONE" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
-    tot = [0, 0, 0, 0]
-    for m in re.finditer(r"\[coop\] bounce \d+ n=\d+ anyhit=(\d+) closest=(\d+) restarts=(\d+) multi=(\d+)", r.stderr):
-        for k in range(4):
+    tot = [0, 0, 0, 0, 0]
+    for m in re.finditer(r"\[coop\] bounce \d+ n=\d+ anyhit=(\d+) closest=(\d+) restarts=(\d+) multi=(\d+) deep=(\d+)",
+                         r.stderr):
+        for k in range(5):
             tot[k] += int(m.group(k + 1))
     return r.stdout, tot
 
@@ -56,20 +57,20 @@ def _run(lib, which, *extra, timeout=400):
 def test_forced_cooperative_finish_fixed_scenes(variant):
     lib = build.variant_path(variant)
     assert os.path.exists(lib), f"variants/libpnrt_{variant}.so not built (__graft_entry__.build())"
-    out, (anyhit, closest, restarts, multi) = _run(lib, "fixed")
+    out, (anyhit, closest, restarts, multi, deep) = _run(lib, "fixed")
     assert "DIAGNOSTIC BUILD" in out
     print(f"{variant}: rays handed over any-hit {anyhit}, closest-hit {closest}, restarts {restarts}, "
-          f"finishes of 2-8 rays together {multi}")
-    assert anyhit > 1000 and closest > 1000 and multi > 100
+          f"finishes of 2-8 rays together {multi}, rays with spilled stack entries {deep}")
+    assert anyhit > 1000 and closest > 1000 and multi > 100 and deep > 0
     assert restarts > (1000 if variant == "coopsmall" else 0)   # (coop: the 65 / 100-triangle leaves)
 
 
 @pytest.mark.parametrize("variant", ["coop", "coopsmall"])
 def test_forced_cooperative_finish_fuzz(variant):
     lib = build.variant_path(variant)
-    out, (anyhit, closest, restarts, multi) = _run(lib, "fuzz")
+    out, (anyhit, closest, restarts, multi, deep) = _run(lib, "fuzz")
     print(f"{variant} fuzz: rays handed over any-hit {anyhit}, closest-hit {closest}, restarts {restarts}, "
-          f"finishes of 2-8 rays together {multi}")
+          f"finishes of 2-8 rays together {multi}, rays with spilled stack entries {deep}")
     assert anyhit > 0 and closest > 0
     if variant == "coopsmall":
         assert restarts > 0
