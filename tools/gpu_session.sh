@@ -13,6 +13,7 @@
 #   tail     WF_TIMING drain census of the lone-frame (D2) trace launches
 #   coopv    the cooperative-finish tests, verbose (hand-over / restart counts)
 #   abd      A/B of prebuilt variants on D2 / D3 synchronised per frame, no HIP events (VARIANTS, ROUNDS)
+#   profd    rocprofv3 kernel trace of D2 / D3 synchronised per frame; tools/frame_gaps.py splits each frame
 #   fuzz     the widened fuzz campaign (SEEDS=40000 random scenes x 3 kernel modes vs the oracle)
 # Output under gpurun_out/$TAG.  Every GPU step has its own time limit; the first failing
 # step ends the session (no retries).
@@ -123,6 +124,13 @@ for s in ${STEPS:-smoke tests bench}; do
       for m in serial pipe; do     # rocprof's trace-kernel average vs the line's kernel_ms (CPU only)
         python3 tools/prof_summary.py $O/prof_$m/run_kernel_trace.csv $O/prof_$m.json $O/prof_${m}_check.json > /dev/null \
           && python3 -c "import json; print('  prof-$m', json.load(open('$O/prof_${m}_check.json'))['check'])"
+      done ;;
+    profd)     # rocprofv3 kernel trace of the reference's dispatch shape, synchronised per frame, no events
+      for c in ${DCONFIGS:-D2 D3}; do
+        step profd-$c timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/profd_$c -o run --output-format csv -- \
+          python bench.py --config $c --sync-per-frame --steps 120 --warmup 16 --no-parity --no-pmc --no-cpu-baseline \
+          --serial-steps 0 --no-kernel-events > $O/profd_$c.json 2> $O/profd_$c.err
+        python3 tools/frame_gaps.py $O/profd_$c/run_kernel_trace.csv | tail -12
       done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
