@@ -295,6 +295,9 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #ifndef WF_STAGGER_PATHS
 #define WF_STAGGER_PATHS 12000000   // (1080p calls of >= 6 frames; a rank's share at N = 2 with 16-frame calls)
 #endif
+#ifndef WF_ALONE_ON_CALLER
+#define WF_ALONE_ON_CALLER 1        // a call with nothing in flight runs on the caller's stream (no worker hop)
+#endif
 #ifndef WF_TRACE_PATHS_PER_BLOCK_ALONE
 #define WF_TRACE_PATHS_PER_BLOCK_ALONE WF_TRACE_BLOCK  // ... for a call with no other call in flight
 #endif
@@ -556,11 +559,16 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         if (Q.primary != old_primary) Q.prim.valid = false;
     }
     ++c->ncall;
-    hipStream_t w = P.w;
+    // A call with nothing in flight runs on the caller's stream itself: no worker
+    // stream to order against it, so no event wait before its first kernel and no
+    // join before its blend (the reference's loop: one frame, then display)
+    const bool on_caller = alone && WF_ALONE_ON_CALLER;
+    hipStream_t w = on_caller ? c->stream : P.w;
     // this pipe's buffers were last read by the blend of the call that used it last
-    if (P.blend_pending) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));
+    // (already complete for a call with nothing in flight: `alone` queried it)
+    if (P.blend_pending && !alone) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));
     // staggered calls: this one starts when the previous one reaches its last bounces
-    if (stagger && prev_pipe != pi && prev_pipe < WF_PIPES && c->pipe[prev_pipe].stage_set)
+    if (stagger && !alone && prev_pipe != pi && prev_pipe < WF_PIPES && c->pipe[prev_pipe].stage_set)
         HIPCHK(c, hipStreamWaitEvent(w, c->pipe[prev_pipe].ev_stage, 0));
     P.stage_set = false;
     // The primary records (camera ray's closest hit per pixel of the shard) depend
@@ -602,13 +610,15 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         a.b.chunk_frames = (int)cf;
         a.b.tiles_x = tiles_x;
         a.b.first_frame = first + f0;
-        if (f0) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));   // the previous group's blend has read the colours
+        if (f0 && w != c->stream) HIPCHK(c, hipStreamWaitEvent(w, P.ev_blend, 0));   // the previous group's blend has read the colours
         const bool last = f0 + cf >= nf;
         if ((rc = render_batch(c, s, fp, a, w, P.primary, P.colors, alone, one, stagger && last ? P.ev_stage : nullptr)))
             return rc;
         if (stagger && last) P.stage_set = true;
-        HIPCHK(c, hipEventRecord(P.ev_join, w));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join, 0));
+        if (w != c->stream) {
+            HIPCHK(c, hipEventRecord(P.ev_join, w));
+            HIPCHK(c, hipStreamWaitEvent(c->stream, P.ev_join, 0));
+        }
         {   // the blends run in call order on the caller's stream
             ProfScope ps(c, PNRT_K_BLEND);
             hipLaunchKernelGGL(pt_blend_kernel, dim3((unsigned)((pix + 255) / 256)), dim3(256), 0, c->stream, fp,
