@@ -97,6 +97,9 @@ def parse(argv=None):
                          "(main.cpp:569-615): a step is one frame")
     ap.add_argument("--sync-per-frame", action="store_true",
                     help="D configs: synchronise after every call (an interactive loop that displays each frame)")
+    ap.add_argument("--sync-with", default="torch", choices=["torch", "pnrt"],
+                    help="--sync-per-frame: wait with torch.cuda.synchronize() (device-wide) or pnrt_synchronize "
+                         "(the library's own streams: what a C caller of the drop-in calls)")
     ap.add_argument("--mode", default="zcull", choices=["exact", "zcull"])
     ap.add_argument("--kernel", default="v3", choices=["v1", "v3"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -620,9 +623,10 @@ def main(argv=None):
     def calls(lo, hi):
         if args.sync_per_frame:             # every frame completed before the next is submitted
             n = 0
+            wait = pt.synchronize if args.sync_with == "pnrt" else torch.cuda.synchronize
             for k in range(lo, hi):
                 n += issue_calls(sf, spp, k, k + 1, ipc, world)
-                torch.cuda.synchronize()
+                wait()
             return n
         return issue_calls(sf, spp, lo, hi, ipc, world)
 
@@ -807,7 +811,7 @@ def main(argv=None):
             "data": "synthetic: procedural stand-in meshes (reference OBJs absent), reference HDR/texture assets",
             "config": {"workload": f"{cfg.name}: {cfg.description}"
                                    + (" -- reference dispatch shape, one pnrt_render per frame"
-                                      + (", synchronised per frame" if args.sync_per_frame else "")
+                                      + (f", synchronised per frame ({args.sync_with})" if args.sync_per_frame else "")
                                       if dispatch_shape else ""), "width": W, "height": H,
                        "spp_per_step": spp, "max_bounce_depth": cfg.max_depth, "triangles": cfg.n_triangles,
                        "iters_per_call": ipc,

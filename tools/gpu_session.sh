@@ -94,7 +94,7 @@ for s in ${STEPS:-smoke tests bench}; do
           for c in ${AB_DCONFIGS:-D2 D3}; do
             step abd-$v-$c-$r env PNRT_DEVICE_LIB=$lib timeout -k 10 200 python bench.py --config $c --sync-per-frame \
               --steps 240 --warmup 16 --no-parity --no-pmc --no-cpu-baseline --serial-steps 0 --no-kernel-events \
-              > $O/abd_${v}_${c}_$r.json 2> $O/abd_${v}_${c}_$r.err
+              ${ABD_ARGS:-} > $O/abd_${v}_${c}_$r.json 2> $O/abd_${v}_${c}_$r.err
             summ $O/abd_${v}_${c}_$r.json
           done
         done
