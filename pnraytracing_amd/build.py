@@ -119,6 +119,12 @@ def build_abi_caller(force=False):
     if force or _stale(out, deps):
         _run(["g++", "-std=c++17", "-O2", "-Wall", "-I", INC, src, "-o", out, "-L", PKG, "-lpnrt", "-lpnrt_host",
               "-Wl,-rpath,$ORIGIN/../../pnraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib"])
+    # the reference's render loop (one pnrt_render per frame) through the C ABI alone, for parity and timing
+    dsrc = os.path.join(REPO, "tests", "abi", "c_abi_dloop.cpp")
+    dout = os.path.join(REPO, "tests", "abi", "c_abi_dloop")
+    if os.path.exists(dsrc) and (force or _stale(dout, deps[1:2] + deps[3:4] + [dsrc])):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-I", INC, dsrc, "-o", dout, "-L", PKG, "-lpnrt",
+              "-Wl,-rpath,$ORIGIN/../../pnraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib"])
     # the multi-GPU caller: one process, one RCCL communicator per device (ncclCommInitAll + ncclGather)
     msrc = os.path.join(REPO, "tests", "abi", "c_abi_multigpu.cpp")
     mout = os.path.join(REPO, "tests", "abi", "c_abi_multigpu")

@@ -181,3 +181,27 @@ def synthetic_c5(width=3840, height=2160, spp=4, nu=2048, nv=1024, env_w=4096, e
 
 
 CONFIGS = {"C1": cornell_c1, "C2": bunny_c2, "C3": marry_c3, "C4": teapot_c4, "C5": synthetic_c5}
+
+
+def export_pnd1(cfg: SceneConfig, path: str) -> None:
+    """Write a scene as the "PND1" file a compiled C caller of the drop-in reads
+    (tests/abi/c_abi_dloop.cpp): the five main.cpp-layout arrays, the frame and
+    camera, the environment and its RandomHDR table, the textures."""
+    p = cfg.packed
+    V, M, T, N, L = (np.ascontiguousarray(a, np.float32) for a in p.arrays())
+    env = cfg.env_rgb is not None
+    eh, ew = (cfg.env_rgb.shape[:2] if env else (0, 0))
+    with open(path, "wb") as f:
+        f.write(b"PND1")
+        f.write(np.array([len(V), len(M), len(T), len(N), len(L)], np.int32).tobytes())
+        f.write(np.array([p.lights_sum_area], np.float32).tobytes())
+        f.write(np.array([cfg.width, cfg.height, cfg.max_depth, ew, eh, len(cfg.textures)], np.int32).tobytes())
+        f.write(np.ascontiguousarray(cfg.camera, np.float32).reshape(12).tobytes())
+        for a in (V, M, T, N, L):
+            f.write(a.tobytes())
+        if env:
+            f.write(np.ascontiguousarray(cfg.env_rgb, np.float32).tobytes())
+            f.write(np.ascontiguousarray(cfg.env_table, np.float32).tobytes())
+        for px, w, h, ch in cfg.textures:
+            f.write(np.array([w, h, ch], np.int32).tobytes())
+            f.write(np.ascontiguousarray(px, np.uint8).reshape(-1).tobytes())

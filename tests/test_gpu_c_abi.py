@@ -67,3 +67,30 @@ def test_compiled_multigpu_caller_gathers_bit_exact(tmp_path, n_shards):
     img = np.fromfile(out, np.float32).reshape(H, W, 4)
     bad = np.argwhere(np.any(img.view(np.uint32) != gold["image"].view(np.uint32), axis=-1))
     assert len(bad) == 0, f"{len(bad)} pixels differ, first {bad[:4].tolist()}"
+
+
+DEXE = os.path.join(HERE, "abi", "c_abi_dloop")
+
+
+@pytest.mark.parametrize("config", ["C2", "C3"])
+def test_compiled_reference_loop_bit_exact(tmp_path, config):
+    """tests/abi/c_abi_dloop: the reference's render loop (one pnrt_render per
+    frame, pnrt_synchronize after each, main.cpp:587-628) from a PND1 scene file
+    (scenes.export_pnd1: arrays, env + RandomHDR table, textures, camera) through
+    the C ABI alone -- the program tools/dloop.py times.  Its image equals the
+    oracle's bit for bit (C2's bunny + env, C3's textures, at 96x64)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    import pyoracle
+    from pnraytracing_amd import scenes as S
+    assert os.path.exists(DEXE), "tests/abi/c_abi_dloop not built (python -c 'import __graft_entry__ as g; g.build()')"
+    cfg = {"C2": S.bunny_c2, "C3": S.marry_c3}[config](width=96, height=64, spp=1)
+    scene, out = str(tmp_path / "s.bin"), str(tmp_path / "out.bin")
+    S.export_pnd1(cfg, scene)
+    for mode in ("sync", "pipe"):
+        r = subprocess.run([DEXE, scene, "5", "3", mode, out], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0 and "ms_per_frame" in r.stdout, r.stdout + r.stderr
+        img = np.fromfile(out, np.float32).reshape(cfg.height, cfg.width, 4)
+        ref, _ = pyoracle.Oracle(cfg).render(0, 8)
+        bad = np.argwhere(np.any(img.view(np.uint32) != ref.view(np.uint32), axis=-1))
+        assert len(bad) == 0, f"{config} {mode}: {len(bad)} pixels differ, first {bad[:4].tolist()}"

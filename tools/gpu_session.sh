@@ -13,6 +13,7 @@
 #   tail     WF_TIMING drain census of the lone-frame (D2) trace launches
 #   coopv    the cooperative-finish tests, verbose (hand-over / restart counts)
 #   abd      A/B of prebuilt variants on D2 / D3 synchronised per frame, no HIP events (VARIANTS, ROUNDS)
+#   dloop    D2 / D3 through the compiled C caller alone (tools/dloop.py), synchronised and pipelined
 #   profd    rocprofv3 kernel trace of D2 / D3 synchronised per frame; tools/frame_gaps.py splits each frame
 #   fuzz     the widened fuzz campaign (SEEDS=40000 random scenes x 3 kernel modes vs the oracle)
 # Output under gpurun_out/$TAG.  Every GPU step has its own time limit; the first failing
@@ -132,6 +133,9 @@ for s in ${STEPS:-smoke tests bench}; do
           --serial-steps 0 --no-kernel-events > $O/profd_$c.json 2> $O/profd_$c.err
         python3 tools/frame_gaps.py $O/profd_$c/run_kernel_trace.csv | tail -12
       done ;;
+    dloop)     # the reference's loop through the C ABI alone (no Python): D2 / D3, synchronised and pipelined
+      step dloop timeout -k 10 300 python tools/dloop.py ${DCONFIGS:-D2 D3} > $O/dloop.json 2> $O/dloop.err
+      cat $O/dloop.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
