@@ -10,7 +10,6 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -295,9 +294,6 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #endif
 #ifndef WF_STAGGER_PATHS
 #define WF_STAGGER_PATHS 12000000   // (1080p calls of >= 6 frames; a rank's share at N = 2 with 16-frame calls)
-#endif
-#ifndef WF_SYNC_SPIN_US
-#define WF_SYNC_SPIN_US 2000        // pnrt_synchronize polls the context's last event this long before blocking
 #endif
 #ifndef WF_ALONE_ON_CALLER
 #define WF_ALONE_ON_CALLER 1        // a call with nothing in flight runs on the caller's stream (no worker hop)
@@ -1272,18 +1268,6 @@ int pnrt_pack_rows(pnrt_ctx* c, void* dst, int band, int nsh, int shard) {
 int pnrt_synchronize(pnrt_ctx* c) {
     if (!c) return PNRT_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    // Every call's work ends on the context stream (its blend, after the join of
-    // the worker stream), where ev_last is recorded last: poll that event for a
-    // short while before blocking -- a loop that waits for every frame (the
-    // reference's one-dispatch-per-frame loop) wakes up as the frame completes
-    // instead of after the blocking wait's wake-up latency.
-    if (WF_SYNC_SPIN_US > 0 && c->last_valid) {
-        const auto t0 = std::chrono::steady_clock::now();
-        hipError_t e;
-        while ((e = hipEventQuery(c->ev_last)) == hipErrorNotReady)
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(WF_SYNC_SPIN_US)) break;
-        if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(c, e);
-    }
     HIPCHK(c, sync_all(c));
     return check_fault(c);
 }
