@@ -73,20 +73,31 @@ int main(int argc, char** argv) {
     if (rc != PNRT_OK) { fprintf(stderr, "setup: %s\n", pnrt_last_error(rt)); return 5; }
 
     // main.cpp:587-628: one dispatch per frame, frameCount++; warm-up frames first
+    double t_render = 0.0, t_sync = 0.0;     // host time inside pnrt_render / pnrt_synchronize (timed frames)
+    bool timed = false;
     auto frame = [&](uint32_t k) -> int {
+        const auto a = std::chrono::steady_clock::now();
         int r = pnrt_render(rt, k, 1, 1, 1, 0);
+        const auto m = std::chrono::steady_clock::now();
         if (r == PNRT_OK && sync) r = pnrt_synchronize(rt);
+        const auto z = std::chrono::steady_clock::now();
+        if (timed) {
+            t_render += std::chrono::duration<double, std::micro>(m - a).count();
+            t_sync += std::chrono::duration<double, std::micro>(z - m).count();
+        }
         return r;
     };
     for (int k = 0; k < warmup && rc == PNRT_OK; ++k) rc = frame((uint32_t)k);
     if (rc == PNRT_OK) rc = pnrt_synchronize(rt);
+    timed = true;
     const auto t0 = std::chrono::steady_clock::now();
     for (int k = warmup; k < warmup + frames && rc == PNRT_OK; ++k) rc = frame((uint32_t)k);
     if (rc == PNRT_OK) rc = pnrt_synchronize(rt);
     const auto t1 = std::chrono::steady_clock::now();
     if (rc != PNRT_OK) { fprintf(stderr, "render: %s\n", pnrt_last_error(rt)); return 8; }
     const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    printf("frames %d mode %s ms_per_frame %.4f width %d height %d\n", frames, sync ? "sync" : "pipe", ms / frames, W, H);
+    printf("frames %d mode %s ms_per_frame %.4f width %d height %d host_render_us %.1f host_sync_us %.1f\n", frames,
+           sync ? "sync" : "pipe", ms / frames, W, H, t_render / frames, t_sync / frames);
     if (argc > 5) {
         std::vector<float> rgba((size_t)W * H * 4);
         if ((rc = pnrt_read_accum(rt, rgba.data()))) { fprintf(stderr, "read_accum: %s\n", pnrt_last_error(rt)); return 9; }

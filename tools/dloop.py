@@ -41,6 +41,8 @@ def main():
                     sys.exit(f"{c} {mode}: rc {r.returncode}: {r.stderr[-2000:]}")
                 ms = float(r.stdout.split("ms_per_frame")[1].split()[0])
                 out[f"ms_per_frame_{mode}"] = ms
+                out[f"host_render_us_{mode}"] = float(r.stdout.split("host_render_us")[1].split()[0])
+                out[f"host_sync_us_{mode}"] = float(r.stdout.split("host_sync_us")[1].split()[0])
                 out[f"msamples_per_s_{mode}"] = round(512 * 512 / ms / 1e3, 2)
             print(json.dumps(out), flush=True)
 
