@@ -935,12 +935,6 @@ PN_DEV bool wf_coop_anyhit(const DevScene& s, const WfBufs& b, __amdgpu_buffer_r
 #ifndef WF_COOP_MAXRAYS
 #define WF_COOP_MAXRAYS 8   // rays finished together (<= 8: the ray table fills row STK, 64 B per ray;
 #endif                      // D2 synchronised: 2 / 4 / 6 / 8 rays 0.654 / 0.625 / 0.611 / 0.605 ms per frame)
-#ifndef WF_COOP_ALL
-#define WF_COOP_ALL 0       // 1: pipelined launches finish their drain the same way (A/B switch; 2: gated)
-#endif
-#ifndef WF_COOP_GATE
-#define WF_COOP_GATE 2      // WF_COOP_ALL 2: waves of the block that must have left first
-#endif
 #define WF_COOP_RAYBITS (WF_COOP_MAXRAYS > 4 ? 3 : 2)      // key bits 63.. : the ray
 #define WF_COOP_RANKSHIFT (64 - WF_COOP_RAYBITS - 7)       // 7 bits below them: the hand-over rank
 static_assert(WF_COOP_MAXRAYS >= 1 && WF_COOP_MAXRAYS <= 8, "the ray table holds at most 8 rays");
@@ -1471,7 +1465,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
             coop_result(WF_DIAG_COOP ? lane == o : busy != 0, res);   // (the owner: the wave's one busy lane in product builds)
         };
         // the rays of lanes `owners` (<= WF_COOP_MAXRAYS, any kinds), one shared frontier
-        constexpr bool MULTI = CC || WF_DIAG_COOP || WF_COOP_ALL;
+        // (pipelined launches keep the one-ray any-hit finish: the multi-ray finish there
+        // measured C2 -1.8 %, C4 -1.0 %, N = 8 shares -3 %, and gated on half the
+        // block's waves having left -2.5 % -- profiles/r05/s3, s12, s13)
+        constexpr bool MULTI = CC || WF_DIAG_COOP;
         auto coop_multi = [&](uint64_t owners) {
             if (WF_DIAG_COOP && lane == 0 && __popcll(owners) > 1) atomicAdd(b.stats + 3, 1ull);
             if (WF_DIAG_COOP && ((owners >> lane) & 1ull) && (t.spa >> WF_SPA_SHIFT) > (uint32_t)STK)
@@ -1507,12 +1504,7 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
         }
         if (WF_COOP_TAIL && !TBL && !WF_STATS) {
             const int nb = __popcll(busym);
-            // (WF_COOP_ALL 2, an A/B switch: pipelined launches too, once WF_COOP_GATE of the
-            // block's waves have left -- the CU is draining, not the wave alone)
-            bool multi_now = MULTI && WF_COOP_TAIL >= 2;
-            if (WF_COOP_ALL >= 2 && !CC && !WF_DIAG_COOP)
-                multi_now = __hip_atomic_load(&bk_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= WF_COOP_GATE;
-            if (multi_now) {
+            if (MULTI && WF_COOP_TAIL >= 2) {
                 // lone calls: once the queue is exhausted -- the drain -- a wave down to
                 // WF_COOP_MAXRAYS rays finishes them with all its lanes together
                 if (exhausted && nb <= WF_COOP_MAXRAYS) {
@@ -1544,7 +1536,6 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                 } else {
                     thr = nb == 1 ? 0 : max(thr, 1);   // come back here when one ray is left
                 }
-                if (WF_COOP_ALL >= 2 && exhausted && nb > 1 && nb <= WF_COOP_MAXRAYS) thr = nb - 1;   // re-check the gate
             }
         }
         // ---- traverse until WF_REFILL_PCT % of the lanes have finished their ray --------
