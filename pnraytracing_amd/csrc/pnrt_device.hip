@@ -403,6 +403,13 @@ static int report_trace_diag(pnrt_ctx* c, const WfBufs& b, hipStream_t st, int b
         fprintf(stderr, "[coop] bounce %d n=%u anyhit=%llu closest=%llu restarts=%llu multi=%llu deep=%llu\n", bounce, b.n,
                 cc[0], cc[1], cc[2], cc[3], cc[4]);
     }
+    if (WF_DIAG_COOPSTAT) {   // the lone calls' drain finish (pt_wf.h): finishes, rays, waves it could not take
+        unsigned long long cc[9];
+        HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipMemcpy(cc, b.stats, sizeof cc, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[coopstat] bounce %d n=%u finishes=%llu rays=%llu deep_stacks=%llu given_back=%llu\n", bounce, b.n,
+                cc[5], cc[8], cc[6], cc[7]);
+    }
     if (WF_STATS) {
         unsigned long long stt[8 + 48];
         HIPCHK(c, hipStreamSynchronize(st));
@@ -445,7 +452,8 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         if (stage && 2 * bounce == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         // segment dequeue counters: zeroed by the setup kernel that queued the rays
         // (the census builds also clear their words)
-        if (WF_STATS || WF_TIMING || WF_DIAG_COOP) HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + 512, st));
+        if (WF_STATS || WF_TIMING || WF_DIAG_COOP || WF_DIAG_COOPSTAT)
+            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + 512, st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)
@@ -455,7 +463,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
             else hipLaunchKernelGGL((pt_wf_trace<WF_STACK, false>), dim3(tg), dim3(WF_TRACE_BLOCK), 0, st, s, b, fp.mode);
         }
         HIPCHK(c, hipGetLastError());
-        if (WF_STATS || WF_TIMING || WF_DIAG_COOP)
+        if (WF_STATS || WF_TIMING || WF_DIAG_COOP || WF_DIAG_COOPSTAT)
             if (int rc = report_trace_diag(c, b, st, bounce, tg)) return rc;
         if (stage && 2 * bounce + 1 == stage_at) HIPCHK(c, hipEventRecord(stage, st));
         {

@@ -29,6 +29,9 @@
 //                   depth-first regime above 8 frontier entries, at most 2 closest-hit
 //                   candidates, keys at most 12 levels below the hand-over -- so the
 //                   -2 restart (the ray traced again by its own lane) happens routinely
+//   WF_DIAG_COOPSTAT  census of the lone calls' drain finish per trace launch: finishes,
+//                   rays finished, waves down to <= 8 rays that could not take it (stack
+//                   entries beyond 64, or a ray given back before) -- "[coopstat]" lines
 // The measured-and-dropped variants and the knockouts of rounds 1-3 (DESIGN.md
 // section 8) live in git history, not here.
 #pragma once
@@ -56,7 +59,10 @@
 #if (WF_DIAG_COOP || WF_DIAG_COOP_SMALL) && !defined(PNRT_DIAG_BUILD)
 #error "WF_DIAG_COOP builds are diagnostic builds: add -DPNRT_DIAG_BUILD"
 #endif
-#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS || WF_DIAG_COOP)
+#ifndef WF_DIAG_COOPSTAT
+#define WF_DIAG_COOPSTAT 0
+#endif
+#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS || WF_DIAG_COOP || WF_DIAG_COOPSTAT)
 
 // Fault words (the context's host-mapped fault area, see pt_wf.h wf_fault)
 #define WF_FAULT_GUARD 0     // a bounded wait of the block-level ray queue ran out (diagnostic builds)

@@ -1512,6 +1512,10 @@ __global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(De
                     uint32_t need = 0;
                     for (uint64_t m = busym; m; m &= m - 1)
                         need += ((uint32_t)__builtin_amdgcn_readlane((int)t.spa, __ffsll((long long)m) - 1) >> WF_SPA_SHIFT) + 2u;
+                    if (WF_DIAG_COOPSTAT && lane == 0) {    // diagnostic census of the drain finish
+                        atomicAdd(b.stats + ((ok && need <= 64u) ? 5 : !ok ? 7 : 6), 1ull);
+                        if (ok && need <= 64u) atomicAdd(b.stats + 8, (unsigned long long)nb);
+                    }
                     if (ok && need <= 64u) {
                         coop_multi(busym);
                         continue;

@@ -21,6 +21,7 @@ from pnraytracing_amd import build
 VARIANTS = {
     "stats": ["-DPNRT_DIAG_BUILD", "-DWF_PIPES=1", "-DWF_STATS=1"],
     "timing": ["-DPNRT_DIAG_BUILD", "-DWF_TIMING=1"],
+    "coopstat": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_COOPSTAT=1"],
     "guard1": build.DIAG_VARIANTS["guard1"],
     "bounds": build.DIAG_VARIANTS["bounds"],
     "pipes1": ["-DWF_PIPES=1"],
