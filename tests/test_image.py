@@ -22,3 +22,17 @@ def test_png_and_pfm_round_trip(tmp_path):
     assert np.array_equal(np.asarray(Image.open(tmp_path / "a.png")), image.to_display(acc))
     image.write_pfm(str(tmp_path / "a.pfm"), acc)
     assert np.array_equal(image.read_pfm(str(tmp_path / "a.pfm")).view(np.uint32), acc[..., :3].view(np.uint32))
+
+
+def test_exr_round_trip(tmp_path):
+    """OpenEXR (uncompressed scanline float, SURVEY 8f row 4's "PNG/EXR writer"):
+    the accumulation image comes back bit for bit, rows in GL order."""
+    rng = np.random.default_rng(2)
+    acc = rng.random((13, 19, 4)).astype(np.float32)
+    acc[3, 4] = (np.inf, -0.0, 1e-40, 7.0)
+    p = str(tmp_path / "a.exr")
+    image.write_exr(p, acc)
+    raw = open(p, "rb").read()
+    assert raw[:4] == b"\x76\x2f\x31\x01" and b"channels\0chlist\0" in raw and b"compression\0compression\0" in raw
+    back = image.read_exr(p)
+    assert back.shape == acc.shape and np.array_equal(back.view(np.uint32), acc.view(np.uint32))
