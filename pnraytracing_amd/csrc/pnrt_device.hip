@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -75,6 +76,8 @@ struct pnrt_ctx {
     int64_t scene_bytes = 0;
     std::vector<int> light_mat;            // material of each light record's triangle (pnrt_update_materials)
     std::vector<float4> light_rec_host;    // host copy of the light records (patched, then one upload)
+    std::vector<float> mat_emit;           // host copy of every material's emission (3 floats each)
+    float env_max = 0.f;                   // largest |texel| component of the env image (NaN: a NaN texel)
     // env + textures
     void* hdr = nullptr;
     void* rnd = nullptr;
@@ -411,9 +414,12 @@ static int report_trace_diag(pnrt_ctx* c, const WfBufs& b, hipStream_t st, int b
                 cc[5], cc[8], cc[6], cc[7]);
     }
     if (WF_STATS) {
-        unsigned long long stt[8 + 48];
+        unsigned long long stt[8 + 48 + 8];
         HIPCHK(c, hipStreamSynchronize(st));
         HIPCHK(c, hipMemcpy(stt, b.stats, sizeof stt, hipMemcpyDeviceToHost));
+        // shadow rays the bounce's setup found moot (pt_wf.h WF_SKIP_MOOT: not traced)
+        fprintf(stderr, "[trace moot] bounce %d light=%llu env=%llu cont=%llu\n", bounce, stt[56], stt[57], stt[58]);
+        HIPCHK(c, hipMemsetAsync(b.stats + 56, 0, 64, st));
         for (int k = 0; k < 3; ++k) {        // lane steps per ray, log2 buckets, by ray kind
             fprintf(stderr, "[trace hist] bounce %d kind %d:", bounce, k);
             for (int q = 0; q < 16; ++q) fprintf(stderr, " %llu", stt[8 + 16 * k + q]);
@@ -440,6 +446,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
     const bool cc = alone && WF_COOP_TAIL >= 2;
     const dim3 g((unsigned)((b.n + 255) / 256));
     b.wr = L.set[0];
+    if (WF_STATS) HIPCHK(c, hipMemsetAsync(b.stats + 56, 0, 64, st));    // the setups' moot-ray counts
     {   // path state + bounce-0 sampling
         ProfScope ps(c, PNRT_K_GEN, st);
         hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
@@ -453,7 +460,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         // segment dequeue counters: zeroed by the setup kernel that queued the rays
         // (the census builds also clear their words)
         if (WF_STATS || WF_TIMING || WF_DIAG_COOP || WF_DIAG_COOPSTAT)
-            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + 512, st));
+            HIPCHK(c, hipMemsetAsync(b.counter, 0, WF_COUNTER_BYTES + (WF_STATS ? 448 : 512), st));
         {
             ProfScope ps(c, PNRT_K_TRACE, st);
             if (s.has_leaf_table)       // (the kernel is instantiated per scene kind)
@@ -760,6 +767,27 @@ int pnrt_set_options(pnrt_ctx* c, int options) {
     return PNRT_OK;
 }
 
+// DevScene::emit_max (pt_wf.h WF_SKIP_MOOT): a bound on every component of the
+// emission a continuation ray can bring back -- any material's, or the env
+// radiance (bilinear taps of the texels: 2^-16 above the largest texel covers the
+// filter's rounding).  A NaN anywhere makes it NaN (then nothing is found moot).
+static float abs_max(const float* v, size_t n, float m) {
+    for (size_t k = 0; k < n; ++k) {
+        const float a = std::fabs(v[k]);
+        if (std::isnan(a) || std::isnan(m)) return std::numeric_limits<float>::quiet_NaN();
+        m = std::max(m, a);
+    }
+    return m;
+}
+static void set_emit_max(pnrt_ctx* c) {
+    float m = abs_max(c->mat_emit.data(), c->mat_emit.size(), 0.f);
+    if (c->scene.has_hdr) {
+        const float e = c->env_max * (1.0f + 0x1p-16f);
+        m = (std::isnan(e) || std::isnan(m)) ? std::numeric_limits<float>::quiet_NaN() : std::max(m, e);
+    }
+    c->scene.emit_max = m;
+}
+
 int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int nm, const float* T, int nt,
                       const float* N, int nn, const float* Lt, int nl, float lsum) {
     if (!c) return PNRT_E_ARG;
@@ -962,6 +990,10 @@ int pnrt_upload_scene(pnrt_ctx* c, const float* V, int nv, const float* M, int n
         s.light_scan = mono ? 1 : 0;
         for (int k = 0; k < WF_LIGHT_SCAN; ++k) s.lscan[k] = k < nl ? lights[k].y : 0.f;
     }
+    c->mat_emit.resize(3 * (size_t)nm);
+    for (int m = 0; m < nm; ++m)
+        for (int k = 0; k < 3; ++k) c->mat_emit[3 * (size_t)m + k] = M[18 * (size_t)m + k];
+    set_emit_max(c);
     c->root_is_leaf = fint(root[7]) == -1;
     c->n_interior = (int)order.size();
     c->max_depth = maxd;
@@ -997,6 +1029,9 @@ int pnrt_update_materials(pnrt_ctx* c, int first, int count, const float* rec) {
     if (lo < hi)
         HIPCHK(c, hipMemcpy(const_cast<float4*>(c->scene.light_rec) + 7 * lo, c->light_rec_host.data() + 7 * lo,
                             (hi - lo) * 7 * sizeof(float4), hipMemcpyHostToDevice));
+    for (int m = 0; m < count; ++m)
+        for (int k = 0; k < 3; ++k) c->mat_emit[3 * (size_t)(first + m) + k] = rec[18 * (size_t)m + k];
+    set_emit_max(c);
     ++c->scene_epoch;                    // primary records hold the hit material's emission
     return PNRT_OK;
 }
@@ -1068,6 +1103,7 @@ int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int 
     HIPCHK(c, sync_all(c));
     free_env(c);
     c->scene.has_hdr = 0;
+    set_emit_max(c);
     ++c->scene_epoch;                    // a primary miss records the env colour
     if (!rgb) return PNRT_OK;
     if (!rnd || w <= 0 || h <= 0) return set_err(c, PNRT_E_ARG, "upload_env: bad arguments");
@@ -1083,6 +1119,8 @@ int pnrt_upload_env(pnrt_ctx* c, const float* rgb, const float* rnd, int w, int 
     if (int rc = env_quads(c, w, h)) return rc;
     c->scene.has_hdr = 1;
     c->scene.hdr_w = w; c->scene.hdr_h = h;
+    c->env_max = abs_max(rgb, 3 * (size_t)w * h, 0.f);
+    set_emit_max(c);
     return PNRT_OK;
 }
 
@@ -1093,6 +1131,7 @@ int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
     HIPCHK(c, sync_all(c));
     free_env(c);
     c->scene.has_hdr = 0;
+    set_emit_max(c);
     ++c->scene_epoch;                    // a primary miss records the env colour
     const size_t n = (size_t)w * h;
     std::vector<float4> a(n);
@@ -1119,6 +1158,8 @@ int pnrt_upload_env_build(pnrt_ctx* c, const float* rgb, int w, int h) {
     if (int rc = env_quads(c, w, h)) return rc;
     c->scene.has_hdr = 1;
     c->scene.hdr_w = w; c->scene.hdr_h = h;
+    c->env_max = abs_max(rgb, 3 * n, 0.f);
+    set_emit_max(c);
     return PNRT_OK;
 }
 

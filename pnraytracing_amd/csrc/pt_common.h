@@ -66,6 +66,7 @@ struct DevScene {
     int light_scan;             // <= PT_LIGHT_SCAN lights with non-decreasing prefix areas
     float lscan[PT_LIGHT_SCAN]; // their prefix areas, passed by value: scalar (kernel-argument) loads
     int has_hdr, hdr_w, hdr_h;
+    float emit_max;             // bound on every |emission| and |env texel| component (NaN: unknown), WF_SKIP_MOOT
     const float4* hdr;          // RGB + pad
     const float4* rnd;          // RandomHDR + pad
     // the same two images as bilinear footprints: record (qj, qi), qi in [0, w],

@@ -266,14 +266,24 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
     return f;
 }
 
+#ifndef WF_SKIP_MOOT
+#define WF_SKIP_MOOT 1        // shadow rays that cannot change the path are not traced (wf_setup_core)
+#endif
+#ifndef WF_MOOT_STASH
+#define WF_MOOT_STASH 2       // where the moot bound waits for dPDF: 0 registers, 2 recomputed from P3 / P4
+#endif
+
 // The light record is always fetched with the material.  ENV_EARLY: the env
 // table taps too (gen; in the shade kernel's setup they cost spills, -1.5 %).
 // SOBOL_PAIR: both Sobol dimensions of the bounce in one pass over the set bits
 // (sobol_pair: shade +1.1 %; in gen, where the bounce is the constant 0 and the
 // per-bit loop folds, it lost 3.5 %).
+// MOOT: the moot shadow-ray test (WF_SKIP_MOOT) -- not in gen: at bounce 0 Lo is
+// zero, so only rays with an exactly zero term are moot (~1.7 % of C2's bounce-0
+// light rays), fewer than the test costs.
 // Returns the ray kinds the bounce emits; writes the path state P0-P7 of entry
 // i of the write set (slot = the path's (pixel, frame) slot); the rays go to `rays`.
-template <bool ENV_EARLY, bool SOBOL_PAIR>
+template <bool ENV_EARLY, bool SOBOL_PAIR, bool MOOT>
 PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const WfBufs& b, uint32_t i, uint32_t slot,
                               int bounce, int x, int py, uint32_t frame, const PathIn& q, BounceRays& rays) {
     const PathSet& w = b.wr;
@@ -353,6 +363,15 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         }
     }
     if (nfl & WF_RENV) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
+    // WF_SKIP_MOOT (below): a bound on the MIS numerator's magnitude, |LE| pe + |LD| pl,
+    // and the denominator's pe + pl
+    f3 mootU = add(mk3(fabsf(LE.x) * fabsf(pe), fabsf(LE.y) * fabsf(pe), fabsf(LE.z) * fabsf(pe)),
+                   mk3(fabsf(LD.x) * fabsf(pl), fabsf(LD.y) * fabsf(pl), fabsf(LD.z) * fabsf(pl)));
+    float mootPL = pe + pl;
+#if WF_MOOT_STASH == 0
+    if constexpr (WF_SKIP_MOOT && MOOT)     // computed here, where LD / LE die
+        asm volatile("" : "+v"(mootU.x), "+v"(mootU.y), "+v"(mootU.z), "+v"(mootPL));
+#endif
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -407,12 +426,85 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     rays.dC = L;
     rays.oP = P;
     rays.oOff = add(P, muls(N, 0.0001f));
-    const uint32_t meta = slot | ((nfl & WF_RLIGHT) ? WF_META_RL : 0u) | ((nfl & WF_RENV) ? WF_META_RE : 0u) |
-                          ((uint32_t)bounce << WF_META_BSHIFT);
     ps_st(w.P0, i, make_float4(rays.oOff.x, rays.oOff.y, rays.oOff.z, dPDF));
-    ps_st(w.P1, i, make_float4(L.x, L.y, L.z, NdotL));
     ps_st(w.P2, i, make_float4(dBRDF.x, dBRDF.y, dBRDF.z, pe));
     ps_st(w.P5, i, make_float4(q.Lo.x, q.Lo.y, q.Lo.z, __uint_as_float(seed)));
+    bool contMoot = false;
+    if constexpr (WF_SKIP_MOOT && MOOT) {
+        // Shadow rays whose outcome cannot change the path are not traced.  A
+        // shadow ray's occlusion reaches nothing but the shade's MIS sum (:936-940),
+        //   Lo + t,  t = (cw * (LE' pe + LD' pl')) * (1 / ((pe + pl') + dPDF)),
+        // with (LD', pl') = (LD, pl) or (0, 0) (light ray unoccluded / occluded,
+        // :890) and LE' = LE or 0 (env ray, :922).  Rounding to nearest is symmetric
+        // and monotone, so |t| of every combination is at most the same chain on
+        // magnitudes, T = |cw| (|LE| pe + |LD| pl) r, with r the larger reciprocal
+        // of |(pe + pl) + dPDF| (light unoccluded) and |(pe + 0) + dPDF| (occluded),
+        // rcp * (1 + 2^-20), above either rounded quotient (a NaN operand reaches T
+        // through the numerator).  Lo + t is monotone in t:
+        // where Lo + T and Lo - T both round back to Lo, every
+        // combination gives Lo's bits (Lo is never -0: it starts at +0 and only
+        // takes round-to-nearest sums, so Lo + (+-0) = Lo) -- the term lies
+        // below Lo's rounding, or cw / LD / LE is zero.  Both rays are then moot:
+        // their meta bits are cleared (the shade adds the "occluded" combination's
+        // term, which leaves Lo), the env ray is not queued, and the light ray
+        // (traced from the path state) gets a NaN direction, which the trace's root
+        // box test rejects.  A NaN or infinite operand (or a zero denominator)
+        // makes T NaN or infinite: no skip.
+        //
+        // The last bounce's continuation ray reaches only the term it adds to the
+        // MIS sum Lo1 (:950-969): ((cw * em) * dBRDF) * NdotL / dPDF, em the hit
+        // material's emission, or the env radiance on a miss (or nothing), every
+        // component within s.emit_max (host: the largest |emission| of any material
+        // and |texel| of the env image).  Tc = ((|cw| emit_max) |dBRDF|) NdotL
+        // rcp(|dPDF|) (1 + 2^-20) bounds it the same way.  The ray is moot where Tc
+        // is 0 (the term is +-0 for every outcome: Lo1 + +-0 = Lo1, Lo1 never -0) or
+        // where Lo1 = Lo is proven (the test above) and Lo + Tc, Lo - Tc round to Lo.
+        // Then P1 gets a NaN direction (the trace misses it) and NdotL = -1 (never
+        // a real value, |N.L| >= 0), which the shade reads as "write Lo1".
+        const bool last = bounce + 1 == fp.max_depth;
+        if ((nfl & (WF_RLIGHT | WF_RENV)) || last) {
+#if WF_MOOT_STASH == 2
+            {   // read back what P3 / P4 just got (same lane, same addresses: in order)
+                asm volatile("" ::: "memory");
+                const float4 r3 = (nfl & WF_RLIGHT) ? w.P3[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 r4 = (nfl & WF_RENV) ? w.P4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                mootU = add(mk3(fabsf(r4.x) * fabsf(pe), fabsf(r4.y) * fabsf(pe), fabsf(r4.z) * fabsf(pe)),
+                            mk3(fabsf(r3.x) * fabsf(r3.w), fabsf(r3.y) * fabsf(r3.w), fabsf(r3.z) * fabsf(r3.w)));
+                mootPL = pe + r3.w;
+            }
+#endif
+            const float r = fmaxf(__builtin_amdgcn_rcpf(fabsf(mootPL + dPDF)),
+                                  __builtin_amdgcn_rcpf(fabsf((pe + 0.f) + dPDF))) * (1.0f + 0x1p-20f);
+            const f3 T = muls(mul(mk3(fabsf(q.cw.x), fabsf(q.cw.y), fabsf(q.cw.z)), mootU), r);
+            const f3 hi = add(q.Lo, T), lo = sub(q.Lo, T);
+            const bool moot = hi.x == q.Lo.x && hi.y == q.Lo.y && hi.z == q.Lo.z && lo.x == q.Lo.x &&
+                              lo.y == q.Lo.y && lo.z == q.Lo.z;
+            if (last) {
+                const float rc = __builtin_amdgcn_rcpf(fabsf(dPDF)) * (1.0f + 0x1p-20f);
+                const f3 Tc = muls(muls(mul(muls(mk3(fabsf(q.cw.x), fabsf(q.cw.y), fabsf(q.cw.z)), s.emit_max),
+                                            mk3(fabsf(dBRDF.x), fabsf(dBRDF.y), fabsf(dBRDF.z))), NdotL), rc);
+                const f3 hc = add(q.Lo, Tc), lc = sub(q.Lo, Tc);
+                contMoot = (Tc.x == 0.f && Tc.y == 0.f && Tc.z == 0.f) ||
+                           (moot && hc.x == q.Lo.x && hc.y == q.Lo.y && hc.z == q.Lo.z && lc.x == q.Lo.x &&
+                            lc.y == q.Lo.y && lc.z == q.Lo.z);
+                if (WF_STATS && contMoot) atomicAdd(&b.stats[58], 1ull);
+            }
+            if (moot && (nfl & (WF_RLIGHT | WF_RENV))) {
+                if (WF_STATS) {     // census builds: moot rays per kind (pnrt_device.hip report_trace_diag)
+                    if (nfl & WF_RLIGHT) atomicAdd(&b.stats[56], 1ull);
+                    if (nfl & WF_RENV) atomicAdd(&b.stats[57], 1ull);
+                }
+                if (nfl & WF_RLIGHT)
+                    ps_st(w.P7, i, make_float4(__uint_as_float(0x7fc00000u), __uint_as_float(0x7fc00000u),
+                                               __uint_as_float(0x7fc00000u), 0.f));
+                nfl &= ~(WF_RLIGHT | WF_RENV);
+            }
+        }
+    }
+    const float qnan = __uint_as_float(0x7fc00000u);
+    ps_st(w.P1, i, contMoot ? make_float4(qnan, qnan, qnan, -1.f) : make_float4(L.x, L.y, L.z, NdotL));
+    const uint32_t meta = slot | ((nfl & WF_RLIGHT) ? WF_META_RL : 0u) | ((nfl & WF_RENV) ? WF_META_RE : 0u) |
+                          ((uint32_t)bounce << WF_META_BSHIFT);
     ps_st(w.P6, i, make_float4(q.cw.x, q.cw.y, q.cw.z, __uint_as_float(meta)));
     return nfl | WF_RCONT;
 }
@@ -505,7 +597,7 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
     const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont);    // compacted path entry
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core<true, false>(s, fp, b, j, i, 0, x, py, frame, q, rays);
+    if (cont) nfl = wf_setup_core<true, false, false>(s, fp, b, j, i, 0, x, py, frame, q, rays);
     wf_enqueue(b, j, nfl, rays, s.n_lights > 0);     // every lane of the wave reaches this point
 }
 
@@ -1696,8 +1788,8 @@ PN_DEV bool wf_shade_path(const DevScene& s, const FrameParams& fp, const WfBufs
     Lo = add(Lo, muls(mul(cw, mis), invPDFSum));
     int lr, k;
     wf_coords(b, slot, x, lr, k);
-    if (ht < 0) {
-        if (s.has_hdr) {
+    if (ht < 0) {      // (a moot continuation ray -- NdotL = -1, WF_SKIP_MOOT -- is a miss that adds nothing)
+        if (s.has_hdr && !(NdotL < 0.f)) {
             f3 enLi = env_color(s, normalize(L));
             Lo = add(Lo, divs(muls(mul(mul(cw, enLi), dBRDF), NdotL), dPDF));
         }
@@ -1751,6 +1843,6 @@ __global__ void __launch_bounds__(256, FINAL ? 8 : WF_SHADE_WAVES) pt_wf_shade_s
     const uint32_t j = blockIdx.x * 256u + wf_entry_rank(cont);
     uint32_t nfl = 0;
     BounceRays rays;
-    if (cont) nfl = wf_setup_core<false, true>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
+    if (cont) nfl = wf_setup_core<false, true, true>(s, fp, b, j, slot, bounce, x, py, frame, q, rays);
     wf_enqueue(b, j, nfl, rays, s.n_lights > 0);     // every lane of the wave reaches this point
 }

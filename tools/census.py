@@ -9,6 +9,10 @@ Requested bytes of one trace launch, in the device layout:
   triangle test   48 B  (the record; the fourth 16-B load of a triangle lane
                          reads one shared address)
   ray             32 B  (origin + direction) + 4 B result
+(rays = every ray the launch took, the moot light rays included: each takes one
+lane step, its root box test; moot_light / moot_env count the shadow rays the
+setup found moot, pt_wf.h WF_SKIP_MOOT -- the env ones are not queued at all --
+and moot_cont the last bounce's continuation rays, NaN rays like the light ones)
 The entry carries the source hash of the sources it was measured on; bench.py
 uses it only while they are unchanged.
 
@@ -25,6 +29,7 @@ sys.path.insert(0, REPO)
 LIB = os.path.join(REPO, "pnraytracing_amd", "variants", "libpnrt_stats.so")
 PAT = re.compile(r"\[trace stats\] bounce (\d+) n=(\d+) iters=(\d+) active/iter=[\d.]+ tri=(\d+) node=(\d+) "
                  r"uniform-fetch iters=(\d+) refills=(\d+) rays=(\d+)")
+MOOT = re.compile(r"\[trace moot\] bounce (\d+) light=(\d+) env=(\d+) cont=(\d+)")
 
 
 def child(name):
@@ -51,6 +56,7 @@ def main(names):
             print(r.stdout[-2000:], r.stderr[-2000:])
             raise SystemExit(f"{name}: census run failed ({r.returncode})")
         b = [tuple(map(int, m.groups())) for m in PAT.finditer(r.stderr)]
+        moot = {int(m.group(1)): (int(m.group(2)), int(m.group(3)), int(m.group(4))) for m in MOOT.finditer(r.stderr)}
         rows = int(re.search(r"rows (\d+) name (\S+)", r.stdout).group(1))
         cname = re.search(r"rows (\d+) name (\S+)", r.stdout).group(2)
         launches = len(b)
@@ -60,7 +66,10 @@ def main(names):
         req = 64 * node + 48 * tri + 36 * rays
         res[cname] = {"source_hash": build.device_source_hash(), "rows": rows, "frames": 4, "trace_launches": launches,
                       "per_bounce": [{"bounce": x[0], "paths": x[1], "iters": x[2], "tri_steps": x[3],
-                                      "node_steps": x[4], "rays": x[7]} for x in b],
+                                      "node_steps": x[4], "rays": x[7],
+                                      "moot_light": moot.get(x[0], (0, 0, 0))[0], "moot_env": moot.get(x[0], (0, 0, 0))[1],
+                                      "moot_cont": moot.get(x[0], (0, 0, 0))[2]}
+                                     for x in b],
                       "lane_steps_per_ray": round((tri + node) / max(rays, 1), 3),
                       "requested_bytes_per_launch": round(req / max(launches, 1))}
         print(cname, {k: v for k, v in res[cname].items() if k != "per_bounce"}, flush=True)
