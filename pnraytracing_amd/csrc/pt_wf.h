@@ -269,8 +269,8 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
 #ifndef WF_SKIP_MOOT
 #define WF_SKIP_MOOT 1        // shadow rays that cannot change the path are not traced (wf_setup_core)
 #endif
-#ifndef WF_MOOT_STASH
-#define WF_MOOT_STASH 2       // where the moot bound waits for dPDF: 0 registers, 2 recomputed from P3 / P4
+#ifndef WF_MOOT_TSUM
+#define WF_MOOT_TSUM 1        // the moot test's bound: T_U + T_E (1), or the numerator over the larger reciprocal (0)
 #endif
 
 // The light record is always fetched with the material.  ENV_EARLY: the env
@@ -363,15 +363,6 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         }
     }
     if (nfl & WF_RENV) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
-    // WF_SKIP_MOOT (below): a bound on the MIS numerator's magnitude, |LE| pe + |LD| pl,
-    // and the denominator's pe + pl
-    f3 mootU = add(mk3(fabsf(LE.x) * fabsf(pe), fabsf(LE.y) * fabsf(pe), fabsf(LE.z) * fabsf(pe)),
-                   mk3(fabsf(LD.x) * fabsf(pl), fabsf(LD.y) * fabsf(pl), fabsf(LD.z) * fabsf(pl)));
-    float mootPL = pe + pl;
-#if WF_MOOT_STASH == 0
-    if constexpr (WF_SKIP_MOOT && MOOT)     // computed here, where LD / LE die
-        asm volatile("" : "+v"(mootU.x), "+v"(mootU.y), "+v"(mootU.z), "+v"(mootPL));
-#endif
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -433,29 +424,29 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     if constexpr (WF_SKIP_MOOT && MOOT) {
         // Shadow rays whose outcome cannot change the path are not traced.  A
         // shadow ray's occlusion reaches nothing but the shade's MIS sum (:936-940),
-        //   Lo + t,  t = (cw * (LE' pe + LD' pl')) * (1 / ((pe + pl') + dPDF)),
+        //   Lo1 = Lo + t,  t = (cw * (LE' pe + LD' pl')) * (1 / ((pe + pl') + dPDF)),
         // with (LD', pl') = (LD, pl) or (0, 0) (light ray unoccluded / occluded,
         // :890) and LE' = LE or 0 (env ray, :922).  Rounding to nearest is symmetric
-        // and monotone, so |t| of every combination is at most the same chain on
-        // magnitudes, T = |cw| (|LE| pe + |LD| pl) r, with r the larger reciprocal
-        // of |(pe + pl) + dPDF| (light unoccluded) and |(pe + 0) + dPDF| (occluded),
-        // rcp * (1 + 2^-20), above either rounded quotient (a NaN operand reaches T
-        // through the numerator).  Lo + t is monotone in t:
-        // where Lo + T and Lo - T both round back to Lo, every
-        // combination gives Lo's bits (Lo is never -0: it starts at +0 and only
-        // takes round-to-nearest sums, so Lo + (+-0) = Lo) -- the term lies
-        // below Lo's rounding, or cw / LD / LE is zero.  Both rays are then moot:
-        // their meta bits are cleared (the shade adds the "occluded" combination's
-        // term, which leaves Lo), the env ray is not queued, and the light ray
-        // (traced from the path state) gets a NaN direction, which the trace's root
-        // box test rejects.  A NaN or infinite operand (or a zero denominator)
-        // makes T NaN or infinite: no skip.
+        // and monotone, so |t| is at most the same chain on magnitudes in the same
+        // order: T_U = (|cw| (|LE| pe + |LD| pl)) rU for the light-unoccluded
+        // outcomes, T_E = (|cw| |LE| pe) rE for the occluded ones, each reciprocal
+        // (of |(pe + pl) + dPDF|, |(pe + 0) + dPDF|) taken as rcp * (1 + 2^-20),
+        // above the rounded quotient; T = T_U + T_E >= both (a sum, so a NaN in
+        // either reaches T).  Lo + t is monotone in t: where Lo + T and Lo - T both
+        // round back to Lo, every outcome gives Lo's bits (Lo is never -0: it starts
+        // at +0 and only takes round-to-nearest sums, so Lo + (+-0) = Lo) -- the term
+        // lies below Lo's rounding, or cw / LD / LE is zero.  Both rays are then
+        // moot: their meta bits are cleared (the shade adds the "occluded" term,
+        // which leaves Lo), the env ray is not queued, and the light ray (traced from
+        // the path state) gets a NaN direction, which the trace's root box test
+        // rejects.  A NaN or infinite operand, or a zero denominator, makes T NaN or
+        // infinite: no skip.
         //
-        // The last bounce's continuation ray reaches only the term it adds to the
-        // MIS sum Lo1 (:950-969): ((cw * em) * dBRDF) * NdotL / dPDF, em the hit
-        // material's emission, or the env radiance on a miss (or nothing), every
-        // component within s.emit_max (host: the largest |emission| of any material
-        // and |texel| of the env image).  Tc = ((|cw| emit_max) |dBRDF|) NdotL
+        // The last bounce's continuation ray reaches only the term it adds to Lo1
+        // (:950-969): ((cw * em) * dBRDF) * NdotL / dPDF, em the hit material's
+        // emission, or the env radiance on a miss (or nothing), every component
+        // within s.emit_max (host: the largest |emission| of any material and
+        // |texel| of the env image).  Tc = (((|cw| emit_max) |dBRDF|) NdotL)
         // rcp(|dPDF|) (1 + 2^-20) bounds it the same way.  The ray is moot where Tc
         // is 0 (the term is +-0 for every outcome: Lo1 + +-0 = Lo1, Lo1 never -0) or
         // where Lo1 = Lo is proven (the test above) and Lo + Tc, Lo - Tc round to Lo.
@@ -463,26 +454,29 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         // a real value, |N.L| >= 0), which the shade reads as "write Lo1".
         const bool last = bounce + 1 == fp.max_depth;
         if ((nfl & (WF_RLIGHT | WF_RENV)) || last) {
-#if WF_MOOT_STASH == 2
-            {   // read back what P3 / P4 just got (same lane, same addresses: in order)
-                asm volatile("" ::: "memory");
-                const float4 r3 = (nfl & WF_RLIGHT) ? w.P3[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 r4 = (nfl & WF_RENV) ? w.P4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                mootU = add(mk3(fabsf(r4.x) * fabsf(pe), fabsf(r4.y) * fabsf(pe), fabsf(r4.z) * fabsf(pe)),
-                            mk3(fabsf(r3.x) * fabsf(r3.w), fabsf(r3.y) * fabsf(r3.w), fabsf(r3.z) * fabsf(r3.w)));
-                mootPL = pe + r3.w;
-            }
+            // the candidates read back from what P3 / P4 just got (same lane, same
+            // addresses: in order) -- held in registers through the BRDF sample they
+            // cost the kernel two spills
+            asm volatile("" ::: "memory");
+            const float4 r3 = (nfl & WF_RLIGHT) ? w.P3[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 r4 = (nfl & WF_RENV) ? w.P4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const f3 acw = mk3(fabsf(q.cw.x), fabsf(q.cw.y), fabsf(q.cw.z));
+            const f3 mE = mk3(fabsf(r4.x) * fabsf(pe), fabsf(r4.y) * fabsf(pe), fabsf(r4.z) * fabsf(pe));
+            const f3 mU = add(mE, mk3(fabsf(r3.x) * fabsf(r3.w), fabsf(r3.y) * fabsf(r3.w), fabsf(r3.z) * fabsf(r3.w)));
+            const float rU = __builtin_amdgcn_rcpf(fabsf((pe + r3.w) + dPDF)) * (1.0f + 0x1p-20f);
+            const float rE = __builtin_amdgcn_rcpf(fabsf((pe + 0.f) + dPDF)) * (1.0f + 0x1p-20f);
+#if WF_MOOT_TSUM
+            const f3 T = add(muls(mul(acw, mU), rU), muls(mul(acw, mE), rE));
+#else
+            const f3 T = muls(mul(acw, mU), fmaxf(rU, rE));     // (looser: the light term over rE)
 #endif
-            const float r = fmaxf(__builtin_amdgcn_rcpf(fabsf(mootPL + dPDF)),
-                                  __builtin_amdgcn_rcpf(fabsf((pe + 0.f) + dPDF))) * (1.0f + 0x1p-20f);
-            const f3 T = muls(mul(mk3(fabsf(q.cw.x), fabsf(q.cw.y), fabsf(q.cw.z)), mootU), r);
             const f3 hi = add(q.Lo, T), lo = sub(q.Lo, T);
             const bool moot = hi.x == q.Lo.x && hi.y == q.Lo.y && hi.z == q.Lo.z && lo.x == q.Lo.x &&
                               lo.y == q.Lo.y && lo.z == q.Lo.z;
             if (last) {
                 const float rc = __builtin_amdgcn_rcpf(fabsf(dPDF)) * (1.0f + 0x1p-20f);
-                const f3 Tc = muls(muls(mul(muls(mk3(fabsf(q.cw.x), fabsf(q.cw.y), fabsf(q.cw.z)), s.emit_max),
-                                            mk3(fabsf(dBRDF.x), fabsf(dBRDF.y), fabsf(dBRDF.z))), NdotL), rc);
+                const f3 Tc = muls(muls(mul(muls(acw, s.emit_max), mk3(fabsf(dBRDF.x), fabsf(dBRDF.y), fabsf(dBRDF.z))),
+                                        NdotL), rc);
                 const f3 hc = add(q.Lo, Tc), lc = sub(q.Lo, Tc);
                 contMoot = (Tc.x == 0.f && Tc.y == 0.f && Tc.z == 0.f) ||
                            (moot && hc.x == q.Lo.x && hc.y == q.Lo.y && hc.z == q.Lo.z && lc.x == q.Lo.x &&
