@@ -335,19 +335,23 @@ def cpu_baseline_c1(cpu: dict):
 
 
 def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26) -> int:
-    """4-spp iterations per pnrt_render call: as given, else as many as fit one
-    batch, at most 4 (16 frames; a batch holds at most 16 frames and 2^26 path
-    slots: 1080p frames and multi-GPU shares 4, a whole 4K frame 2).  Multi-rank
-    runs pass the LARGEST share (ShardedFrame.max_rows), so every rank issues the
-    same calls and therefore the same gathers (batch_slots: a test override).  A call's
-    primary pass and each trace launch's drain are fixed costs, and a rank of N
-    GPUs renders 1/N of the rows: against 8-frame calls the one-GPU shard
-    simulation gives per rank +4 % at N = 2, +3 % at N = 4, +9 % at N = 8; on the
-    whole 1080p frame (N = 1) the two measure the same within 1 %."""
+    """4-spp iterations per pnrt_render call: as given, else calls of about a whole
+    1080p frame's 16 frames of paths (2^21 paths per frame x 16, rounded down to a
+    power-of-two multiple of 16 frames: 16 frames of a 1080p frame, 32 of a half,
+    64 -- the most a batch holds -- of a quarter or less), and no more frames than
+    one batch's 2^26 path slots take (a whole 4K frame: 8).  Multi-rank runs pass
+    the LARGEST share (ShardedFrame.max_rows), so every rank issues the same calls
+    and therefore the same gathers (batch_slots: a test override).  A call's primary
+    pass, each trace launch's drain and its gather are fixed costs, and a rank of
+    N GPUs renders 1/N of the rows: in the driver's 20-step region
+    (tools/share_bench.py, rank 0's share alone, profiles/r05/s24) 16-frame calls
+    gave a rank 1 542 / 1 667 / 1 792 Msamples/s at N = 8 / 4 / 2 (N = 1: 1 812);
+    64-frame calls 1 688 / 1 773 / 1 811, 32-frame ones at N = 2 1 791-1 813."""
     if args.iters_per_call > 0:
         return args.iters_per_call
-    frames = min(16, batch_slots // max(1, paths_per_frame))
-    return max(1, min(4, frames // 4))
+    scale = max(1, min(4, (1 << 21) // max(1, paths_per_frame)))
+    frames = min(16 * scale, batch_slots // max(1, paths_per_frame))
+    return max(1, min(16, frames // 4))
 
 
 def call_groups(lo: int, hi: int, ipc: int):

@@ -242,8 +242,8 @@ static int prof_collect(pnrt_ctx* c) {
 }
 
 #ifndef WF_MAX_CHUNK_FRAMES
-#define WF_MAX_CHUNK_FRAMES 16   // frames per batch at most (a call of up to four 4-spp iterations of a
-                                 // 1080p frame or share is one batch)
+#define WF_MAX_CHUNK_FRAMES 64   // frames per batch at most (bench.py's calls: 16 frames of a 1080p frame,
+                                 // 32 / 64 of a multi-GPU rank's half / quarter or smaller share, one batch each)
 #endif
 
 static int grow(pnrt_ctx* c, void** p, size_t* cap, size_t bytes) {
@@ -506,7 +506,7 @@ static int pipes_init(pnrt_ctx* c) {
 }
 
 // v3 wavefront, one pnrt_render call on a pipe: the primary pass (unless the
-// pipe's records are still valid, PrimKey), then per group of <= 16 frames one
+// pipe's records are still valid, PrimKey), then per group of <= WF_MAX_CHUNK_FRAMES frames one
 // batch (gen -> {trace -> shade} x depth) on the pipe's worker stream, then the
 // frame-ordered blend on the context stream.  Consecutive calls are independent
 // path sets, so running them concurrently changes nothing in the result; the

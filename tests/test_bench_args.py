@@ -19,10 +19,11 @@ def test_iters_per_call_defaults():
     b = _bench()
     ns = type("A", (), {"iters_per_call": 0})()
     assert b.iters_per_call(ns, 1920 * 1080) == 4          # 16 frames of 1080p: one batch
-    for n in (2, 4, 8):
-        assert b.iters_per_call(ns, 1920 * (1080 // n)) == 4   # multi-GPU shares
+    assert b.iters_per_call(ns, 1920 * 540) == 8           # N = 2 shares: 32 frames
+    for n in (4, 8):
+        assert b.iters_per_call(ns, 1920 * (1080 // n)) == 16  # N = 4, 8: 64 frames, a batch's most
     assert b.iters_per_call(ns, 3840 * 2160) == 2          # 4K: 8 frames per batch
-    assert b.iters_per_call(ns, 3840 * 270) == 4           # a rank's 4K share at N = 8
+    assert b.iters_per_call(ns, 3840 * 270) == 8           # a rank's 4K share at N = 8: 32 frames
     assert b.iters_per_call(ns, 8192 * 4320) == 1          # one frame per batch
     ns.iters_per_call = 3
     assert b.iters_per_call(ns, 1920 * 1080) == 3 and b.iters_per_call(ns, 3840 * 2160) == 3
