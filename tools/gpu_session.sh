@@ -59,7 +59,7 @@ for s in ${STEPS:-smoke tests bench}; do
           2> $O/tail_$c.err
       done ;;
     shard)     # the multi-GPU share simulation: rank 0's rows of an N-way split on one GPU (16-frame calls)
-      step shard env GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python tools/shard_sim.py 30 16 > $O/shard_sim.txt 2>&1
+      step shard env GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python tools/shard_sim.py 30 ${SHARD_FPC:-auto} > $O/shard_sim.txt 2>&1
       cat $O/shard_sim.txt ;;
     fuzz)
       step fuzz env PNRT_FUZZ_SEEDS=${SEEDS:-40000} timeout -k 10 1100 python -u -m pytest tests/test_gpu_fuzz.py -x -q \
