@@ -824,7 +824,11 @@ def main(argv=None):
                        "primary": ("reused across calls (camera fixed): each pipe keeps its primary records while "
                                    "camera / frame / shard / mode / scene are unchanged, so the timed steps trace "
                                    "no primary pass (exact: no camera jitter, ray_tracing.comp:980; DESIGN.md "
-                                   "section 15)")},
+                                   "section 15)"),
+                       "moot_rays": ("shadow rays, and the last bounce's continuation rays, whose outcome is proven "
+                                     "per ray not to change the path's radiance bits (monotone rounding bound on the "
+                                     "MIS / emission term) are not traced; every timed image is checked against the "
+                                     "oracle, which traces them all (DESIGN.md section 16)")},
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
                                                requested["frac_of_l2"] if requested else None, ghit),
                          "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "
