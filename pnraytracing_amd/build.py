@@ -88,7 +88,9 @@ def build_device(force=False, extra=()):
 DIAG_VARIANTS = {"guard1": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_GUARD=1"],
                  "bounds": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_BOUNDS=1"],
                  "coop": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_COOP=24", "-DWF_DIAG_BOUNDS=1"],
-                 "coopsmall": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_COOP=24", "-DWF_DIAG_COOP_SMALL=1", "-DWF_DIAG_BOUNDS=1"]}
+                 "coopsmall": ["-DPNRT_DIAG_BUILD", "-DWF_DIAG_COOP=24", "-DWF_DIAG_COOP_SMALL=1", "-DWF_DIAG_BOUNDS=1"],
+                 # the trace census (tools/census.py; moot-ray counts, tests/test_gpu_moot.py)
+                 "stats": ["-DPNRT_DIAG_BUILD", "-DWF_PIPES=1", "-DWF_STATS=1"]}
 
 
 def variant_path(name: str) -> str:

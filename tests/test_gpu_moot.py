@@ -66,3 +66,49 @@ def test_emission_edit_moves_the_bound(scale):
         pt.update_materials(0, edited)
         pt.render(2, 3)
         assert _bitwise(pt.read_accum(), ref) == 0
+
+
+_CHILD = r"""
+import sys
+sys.path.insert(0, {repo!r}); sys.path.insert(0, {oracle!r})
+import numpy as np
+import pyoracle
+from pnraytracing_amd import scenes as S
+from pnraytracing_amd.tracer import PathTracer
+cfg = S.bunny_c2(96, 64, spp=4)
+with PathTracer(0) as pt:
+    print("LIB", pt.version(), flush=True)
+    pt.load(cfg)
+    pt.reset_accum()
+    pt.render(0, 4)
+    got = pt.read_accum()
+ref, _ = pyoracle.Oracle(cfg).render(0, 4)
+bad = int(np.count_nonzero(np.any(got.view(np.uint32) != ref.view(np.uint32), axis=-1)))
+print("DIFFERING", bad, flush=True)
+"""
+
+
+def test_moot_rays_are_skipped_and_counted():
+    """The census build (build.py DIAG_VARIANTS "stats") counts, per bounce, the
+    light, env and last-bounce continuation rays its setup found moot: on C2
+    (lights, env, depth 4) all three kinds occur, bounce 0 (gen: no test) has
+    none, and the image still equals the oracle's."""
+    import os
+    import re
+    import subprocess
+    import sys
+    from pnraytracing_amd import build
+    lib = build.variant_path("stats")
+    assert os.path.exists(lib), "variants/libpnrt_stats.so not built (__graft_entry__.build())"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _CHILD.format(repo=repo, oracle=os.path.join(repo, "oracle"))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PNRT_DEVICE_LIB=lib),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "DIAGNOSTIC" in r.stdout and "DIFFERING 0" in r.stdout, r.stdout[-1000:]
+    moot = {int(m.group(1)): tuple(map(int, m.group(2, 3, 4))) for m in
+            re.finditer(r"\[trace moot\] bounce (\d+) light=(\d+) env=(\d+) cont=(\d+)", r.stderr)}
+    assert sorted(moot) == [0, 1, 2, 3], r.stderr[-2000:]
+    assert moot[0] == (0, 0, 0)
+    assert sum(v[0] for v in moot.values()) > 0 and sum(v[1] for v in moot.values()) > 0
+    assert moot[3][2] > 0 and all(moot[b][2] == 0 for b in (1, 2))
