@@ -440,7 +440,8 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         // which leaves Lo), the env ray is not queued, and the light ray (traced from
         // the path state) gets a NaN direction, which the trace's root box test
         // rejects.  A NaN or infinite operand, or a zero denominator, makes T NaN or
-        // infinite: no skip.
+        // infinite: no skip; nor is there one where a reciprocal falls below 2^-126
+        // (where v_rcp_f32 may return 0, no bound).
         //
         // The last bounce's continuation ray reaches only the term it adds to Lo1
         // (:950-969): ((cw * em) * dBRDF) * NdotL / dPDF, em the hit material's
@@ -471,16 +472,19 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
             const f3 T = muls(mul(acw, mU), fmaxf(rU, rE));     // (looser: the light term over rE)
 #endif
             const f3 hi = add(q.Lo, T), lo = sub(q.Lo, T);
-            const bool moot = hi.x == q.Lo.x && hi.y == q.Lo.y && hi.z == q.Lo.z && lo.x == q.Lo.x &&
-                              lo.y == q.Lo.y && lo.z == q.Lo.z;
+            // (a reciprocal below 2^-126 -- a denominator above 2^126 -- may come back
+            // flushed to 0 from v_rcp_f32 and bound nothing: no skip)
+            const bool moot = rU >= 0x1p-126f && rE >= 0x1p-126f && hi.x == q.Lo.x && hi.y == q.Lo.y &&
+                              hi.z == q.Lo.z && lo.x == q.Lo.x && lo.y == q.Lo.y && lo.z == q.Lo.z;
             if (last) {
                 const float rc = __builtin_amdgcn_rcpf(fabsf(dPDF)) * (1.0f + 0x1p-20f);
                 const f3 Tc = muls(muls(mul(muls(acw, s.emit_max), mk3(fabsf(dBRDF.x), fabsf(dBRDF.y), fabsf(dBRDF.z))),
                                         NdotL), rc);
                 const f3 hc = add(q.Lo, Tc), lc = sub(q.Lo, Tc);
-                contMoot = (Tc.x == 0.f && Tc.y == 0.f && Tc.z == 0.f) ||
-                           (moot && hc.x == q.Lo.x && hc.y == q.Lo.y && hc.z == q.Lo.z && lc.x == q.Lo.x &&
-                            lc.y == q.Lo.y && lc.z == q.Lo.z);
+                contMoot = rc >= 0x1p-126f &&
+                           ((Tc.x == 0.f && Tc.y == 0.f && Tc.z == 0.f) ||
+                            (moot && hc.x == q.Lo.x && hc.y == q.Lo.y && hc.z == q.Lo.z && lc.x == q.Lo.x &&
+                             lc.y == q.Lo.y && lc.z == q.Lo.z));
                 if (WF_STATS && contMoot) atomicAdd(&b.stats[58], 1ull);
             }
             if (moot && (nfl & (WF_RLIGHT | WF_RENV))) {

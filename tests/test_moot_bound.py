@@ -41,9 +41,9 @@ def _moot(Lo, cw, LD, pl, LE, pe, dPDF, tsum=True):
         mE = np.abs(LE) * np.abs(pe)[:, None]
         mU = mE + np.abs(LD) * np.abs(pl)[:, None]
 
-        def rcp_low(d):     # v_rcp_f32 within 1 ulp: the quotient one ulp toward zero
-            q = F(1.0) / np.abs(d)
-            return np.nextafter(q, F(0.0)).astype(F)
+        def rcp_low(d):     # v_rcp_f32 within 1 ulp: the quotient one ulp toward zero; a
+            q = F(1.0) / np.abs(d)          # subnormal result may come back flushed to 0
+            return np.where(q < F(2.0 ** -126), F(0.0), np.nextafter(q, F(0.0))).astype(F)
 
         rU = rcp_low((pe + pl) + dPDF) * (F(1.0) + F(2.0 ** -20))
         rE = rcp_low((pe + F(0.0)) + dPDF) * (F(1.0) + F(2.0 ** -20))
@@ -52,7 +52,8 @@ def _moot(Lo, cw, LD, pl, LE, pe, dPDF, tsum=True):
         else:
             T = (acw * mU) * np.fmax(rU, rE)[:, None]
         hi, lo = Lo + T, Lo - T
-        return np.all((hi == Lo) & (lo == Lo), axis=1)
+        ok = (rU >= F(2.0 ** -126)) & (rE >= F(2.0 ** -126))
+        return ok & np.all((hi == Lo) & (lo == Lo), axis=1)
 
 
 def _draw(rng, n, shape=()):
@@ -111,6 +112,9 @@ def test_moot_edge_cases():
         (one * 1.0, one * 1.0, one * 2.0 ** -20, 1.0, one * 0.0, 0.0, 1.0, False),
         (one * 0.0, one * 1.0, one * 0.0, 3.0, one * 0.0, 0.0, 0.5, True),       # dark light, no env term
         (one * 0.0, one * 1.0, one * 0.0, 3.0, one * 1e-30, 0.2, 0.5, False),
+        # a denominator above 2^126: the reciprocal may flush to 0 and bound nothing
+        (one * 0.0, one * 1.0, one * 1.0, 1e38, one * 0.0, 0.0, 0.5, False),
+        (one * 0.0, one * 0.5, one * 0.0, 1.0, one * 0.0, 0.0, 3e38, False),
     ]
     for Lo, cw, LD, pl, LE, pe, dPDF, want in cases:
         args = [np.asarray(v, F) for v in (Lo, cw, LD)] + [np.array([pl], F)] + [np.asarray(LE, F)] + \
@@ -128,11 +132,11 @@ def _cont_moot(Lo, cw, E, dBRDF, NdotL, dPDF, mis_same):
     Lo +- Tc round to Lo."""
     with np.errstate(all="ignore"):
         q = F(1.0) / np.abs(dPDF)
-        rc = np.nextafter(q, F(0.0)).astype(F) * (F(1.0) + F(2.0 ** -20))
+        rc = np.where(q < F(2.0 ** -126), F(0.0), np.nextafter(q, F(0.0))).astype(F) * (F(1.0) + F(2.0 ** -20))
         Tc = (((np.abs(cw) * E[:, None]) * np.abs(dBRDF)) * NdotL[:, None]) * rc[:, None]
         zero = np.all(Tc == 0, axis=1)
         near = np.all((Lo + Tc == Lo) & (Lo - Tc == Lo), axis=1)
-        return zero | (mis_same & near)
+        return (rc >= F(2.0 ** -126)) & (zero | (mis_same & near))
 
 
 def test_last_bounce_continuation_moot():
