@@ -7,7 +7,9 @@ test to its ends, each against the oracle bit for bit (tolerance 0 ulp):
 * the light's emission raised a millionfold by pnrt_update_materials after
   frames were rendered with it tiny -- the library's emission bound must follow
   the edit, or last-bounce rays that now hit a bright light would be skipped;
-* the reverse edit (bright to dark).
+* the reverse edit (bright to dark);
+* the environment dimmed / brightened by 10^6, then the original uploaded
+  between frames (the bound includes the env's largest texel).
 The hand-picked and random float cases of the bound itself are in
 tests/test_moot_bound.py (CPU)."""
 import numpy as np
@@ -64,6 +66,27 @@ def test_emission_edit_moves_the_bound(scale):
         pt.render(0, 2)
         pt.synchronize()
         pt.update_materials(0, edited)
+        pt.render(2, 3)
+        assert _bitwise(pt.read_accum(), ref) == 0
+
+
+@pytest.mark.parametrize("scale", [1e6, 1e-6])
+def test_env_upload_moves_the_bound(scale):
+    """The emission bound follows pnrt_upload_env too: C2 (env-lit) rendered
+    with its environment dimmed (or brightened) by 10^6, then the original
+    environment uploaded between frames (same importance table both times)."""
+    import dataclasses
+    full = S.bunny_c2(96, 64, spp=4)
+    other = dataclasses.replace(full, env_rgb=(full.env_rgb / np.float32(scale)).astype(np.float32))
+    ref = np.zeros((64, 96, 4), np.float32)
+    pyoracle.Oracle(other).render(0, 2, accum=ref)
+    pyoracle.Oracle(full).render(2, 3, accum=ref)
+    with PathTracer(0) as pt:
+        pt.load(other)
+        pt.reset_accum()
+        pt.render(0, 2)
+        pt.synchronize()
+        pt.upload_env(full.env_rgb, full.env_table)
         pt.render(2, 3)
         assert _bitwise(pt.read_accum(), ref) == 0
 
