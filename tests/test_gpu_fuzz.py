@@ -77,8 +77,12 @@ def pt():
         yield t
 
 
-# PNRT_FUZZ_SEEDS=N widens the campaign (default 24 seeds; 400 were run once)
-@pytest.mark.parametrize("seed", list(range(int(os.environ.get("PNRT_FUZZ_SEEDS", "24")))))
+# PNRT_FUZZ_SEEDS=N widens the campaign (default 24 seeds; 400 were run once),
+# PNRT_FUZZ_FIRST=k starts it at seed k (a fresh range)
+_FIRST = int(os.environ.get("PNRT_FUZZ_FIRST", "0"))
+
+
+@pytest.mark.parametrize("seed", list(range(_FIRST, _FIRST + int(os.environ.get("PNRT_FUZZ_SEEDS", "24")))))
 def test_random_scene_bitwise(pt, seed):
     from pnraytracing_amd.tracer import KERNEL_V1, TRAVERSE_EXACT, TRAVERSE_ZCULL
     cfg, rng = random_scene(seed)

@@ -62,7 +62,7 @@ for s in ${STEPS:-smoke tests bench}; do
       step shard env GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python tools/shard_sim.py 30 ${SHARD_FPC:-auto} > $O/shard_sim.txt 2>&1
       cat $O/shard_sim.txt ;;
     fuzz)
-      step fuzz env PNRT_FUZZ_SEEDS=${SEEDS:-40000} timeout -k 10 1100 python -u -m pytest tests/test_gpu_fuzz.py -x -q \
+      step fuzz env PNRT_FUZZ_SEEDS=${SEEDS:-40000} PNRT_FUZZ_FIRST=${FIRST:-0} timeout -k 10 1100 python -u -m pytest tests/test_gpu_fuzz.py -x -q \
         --timeout 300 --timeout-method thread > $O/fuzz.log 2>&1
       tail -2 $O/fuzz.log ;;
     bench)
