@@ -163,3 +163,26 @@ def test_nonfinite_box_disables_culling(pt):
         pt.render(0, 3)
         got = pt.read_accum()
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), mode
+
+
+@pytest.mark.parametrize("seed,exp10", [(200 + k, (-30, -20, -10, 10, 20, 25)[k % 6]) for k in range(48)])
+def test_random_scene_extreme_emission(pt, seed, exp10):
+    """Emission scaled by 10^exp10 (every emissive material): radiance terms far
+    below or above Lo's rounding, subnormal products at 1e-30 -- where the moot-ray
+    test (pt_wf.h WF_SKIP_MOOT) decides most often; still bit for bit."""
+    import dataclasses
+    from pnraytracing_amd.tracer import TRAVERSE_ZCULL
+    cfg, rng = random_scene(seed)
+    mats = cfg.packed.materials.copy()
+    mats[:, 0:3] = (mats[:, 0:3].astype(np.float64) * 10.0 ** exp10).astype(np.float32)
+    cfg = dataclasses.replace(cfg, packed=dataclasses.replace(cfg.packed, materials=mats),
+                              max_depth=4)
+    first, n = int(rng.integers(0, 20)), 6
+    ref, _ = pyoracle.Oracle(cfg).render(first, n)
+    assert np.isfinite(ref).all()
+    pt.load(cfg, TRAVERSE_ZCULL)
+    pt.reset_accum()
+    pt.render(first, n)
+    got = pt.read_accum()
+    bad = np.any(got.view(np.uint32) != ref.view(np.uint32), axis=-1)
+    assert not bad.any(), f"seed {seed} x1e{exp10}: {int(bad.sum())} of {bad.size} pixels differ"
