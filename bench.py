@@ -80,8 +80,15 @@ L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 (8 XCDs) ~34.5 TB/s
 # reported at 2 x FETCH_SIZE, an upper bound.
 STREAM_FACTOR, GATHER_FACTOR = 2.0, 1.0
 CALIBRATION = "profiles/r03/fetch_calibration.json"
-# rocprofv3 --pmc passes (one run each; TCC block: FETCH_SIZE uses 3 counters, WRITE_SIZE 2)
-PMC_PASSES = [("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum")]
+# rocprofv3 --pmc passes (one run each; TCC block: FETCH_SIZE uses 3 counters, WRITE_SIZE 2; the third
+# pass: 6 SQ, 1 GRBM and 1 TA counter, within the 8 / 2 / 2 a pass may hold)
+PMC_PASSES = [("FETCH_SIZE",), ("WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"),
+              ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES",
+               "GRBM_GUI_ACTIVE", "TA_BUSY_avr")]
+# VALU issue: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles (MI355X_MICROARCH.md); 1024
+# SIMDs; GRBM_GUI_ACTIVE is reported summed over the 8 XCDs (per-XCD busy cycles = value / 8)
+N_SIMD, N_XCD, VALU_CYC = 1024, 8, 2.0
+VALU_BOUND = 0.6       # derive_bound: "valu-issue" when the kernel issues VALU on >= this share of SIMD cycles
 KSHORT = {"pt_wf_trace": "trace", "pt_wf_gen_setup": "gen", "pt_wf_shade_setup": "shade",
           "pt_primary_kernel": "primary", "pt_primary_wf": "primary", "pt_blend_kernel": "blend", "pt_render_kernel": "v1"}
 
@@ -170,6 +177,20 @@ def _read_counters(d):
     return out
 
 
+def pmc_child_cmd(args, shard_world: int, exe: str, group, d: str) -> list:
+    """One PMC pass: rocprofv3 over `bench.py --child` rendering rank 0's share of a
+    shard_world-way split in calls of the timed calls' size (pmc_iters_per_call),
+    2 calls timed after 1 of warm-up."""
+    ipc = pmc_iters_per_call(args, shard_world)
+    cmd = ["timeout", "-s", "KILL", str(args.pmc_timeout), exe, "--kernel-trace", "--pmc", *group,
+           "-d", d, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--child", "--config", args.config, "--mode", args.mode,
+           "--kernel", args.kernel, "--steps", str(2 * ipc), "--warmup", str(ipc)]
+    if args.spp:
+        cmd += ["--spp", str(args.spp)]
+    return cmd + ["--iters-per-call", str(ipc), "--shard-world", str(shard_world)]
+
+
 def live_pmc(args, shard_world: int = 1):
     """Two rocprofv3 --kernel-trace --pmc passes over a short run of this same
     workload (child processes: this process has not touched the GPU yet) -- at
@@ -182,23 +203,18 @@ def live_pmc(args, shard_world: int = 1):
         return None
     tmp = tempfile.mkdtemp(prefix="pnrt_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
-    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", RC_DIR_ENV):
         env.pop(v, None)
-    # whole calls only, so every launch covers the same iterations (the child picks
-    # its own calls: a multiple of 4 iterations is whole calls of 1, 2 or 4)
-    ipc = args.iters_per_call if args.iters_per_call > 0 else 4
+    # whole calls of the TIMED calls' size, so every profiled launch covers the
+    # iterations a timed launch covers: the share's call size computed here exactly
+    # as the child (and the timed run) will compute it, and passed explicitly
+    ipc = pmc_iters_per_call(args, shard_world)
     steps, warm = 2 * ipc, ipc
     counters = {}
     try:
         for i, group in enumerate(PMC_PASSES):
             d = os.path.join(tmp, f"p{i}")
-            cmd = ["timeout", "-s", "KILL", str(args.pmc_timeout), exe, "--kernel-trace", "--pmc", *group,
-                   "-d", d, "-o", "run", "--output-format", "csv", "--",
-                   sys.executable, os.path.abspath(__file__), "--child", "--config", args.config, "--mode", args.mode,
-                   "--kernel", args.kernel, "--steps", str(steps), "--warmup", str(warm)]
-            if args.spp:
-                cmd += ["--spp", str(args.spp)]
-            cmd += ["--iters-per-call", str(args.iters_per_call), "--shard-world", str(shard_world)]
+            cmd = pmc_child_cmd(args, shard_world, exe, group, d)
             log(f"PMC pass {i + 1}/{len(PMC_PASSES)}: {' '.join(group)}")
             t = time.perf_counter()
             with open(os.path.join(tmp, f"p{i}.log"), "w") as lf:
@@ -223,8 +239,53 @@ def live_pmc(args, shard_world: int = 1):
              "launches_per_step": cs["_n"] / (steps + warm)}
         if "TCC_HIT_sum" in cs:
             e["l2_hit_rate"] = cs["TCC_HIT_sum"] / max(cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"], 1.0)
+        e.update(issue_stats(cs))
         res[k] = e
     return res or None
+
+
+def issue_stats(cs):
+    """Issue-side figures of one kernel class from the third PMC pass (averages per
+    dispatch): valu_util = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+    -- the share of SIMD cycles issuing VALU --; ta_busy = TA_BUSY_avr / (GRBM_GUI_ACTIVE /
+    8), the texture-address units' busy share; VALU / SALU per wave; wait_frac =
+    SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)."""
+    out = {}
+    g = cs.get("GRBM_GUI_ACTIVE")
+    if not g:
+        return out
+    cyc = g / N_XCD
+    if "SQ_INSTS_VALU" in cs:
+        out["valu_util"] = cs["SQ_INSTS_VALU"] * VALU_CYC / (N_SIMD * cyc)
+    if "TA_BUSY_avr" in cs:
+        out["ta_busy"] = cs["TA_BUSY_avr"] / cyc
+    w = cs.get("SQ_WAVES")
+    if w:
+        if "SQ_INSTS_VALU" in cs:
+            out["valu_per_wave"] = cs["SQ_INSTS_VALU"] / w
+        if "SQ_INSTS_SALU" in cs:
+            out["salu_per_wave"] = cs["SQ_INSTS_SALU"] / w
+    if cs.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in cs:
+        out["wait_frac"] = cs["SQ_WAIT_ANY"] / cs["SQ_WAVE_CYCLES"]
+    return out
+
+
+CONFIG_DIMS = {"C2": (1920, 1080), "C3": (1920, 1080), "C4": (1920, 1080), "C5": (3840, 2160),
+               "D2": (512, 512), "D3": (512, 512)}
+
+
+def pmc_iters_per_call(args, shard_world: int) -> int:
+    """The iterations per call the PMC child (and the timed run) will use: as given;
+    1 for the D configs (one frame per call); else iters_per_call() of the largest
+    share of a shard_world-way split of the config's rows (ShardedFrame.max_rows)."""
+    if args.iters_per_call > 0:
+        return args.iters_per_call
+    if args.config.startswith("D"):
+        return 1
+    from pnraytracing_amd.tracer import shard_rows      # (numpy only: loads no library)
+    W, H = CONFIG_DIMS[args.config]
+    rows = max(len(shard_rows(H, BAND, shard_world, r)) for r in range(shard_world))
+    return iters_per_call(args, rows * W)
 
 
 def stored_keyed(path, key, src_hash):
@@ -404,9 +465,12 @@ def launches_per_step_of(k_launches: int, steps: int, excl: dict, kname: str):
 L2_HIT_CYC, MISS_CYC = 200.0, 900.0   # MI355X_MICROARCH.md: global_load L2-hit / HBM-miss latency (cycles)
 
 
-def derive_bound(hbm_frac, l2_hit, l2_frac, gather_hit=None):
+def derive_bound(hbm_frac, l2_hit, l2_frac, gather_hit=None, valu_util=None):
     """The roof that binds, from the counters: "hbm" (bandwidth) when the kernel's
-    fabric traffic reaches half the HBM peak; below that the kernel is bound by
+    fabric traffic reaches half the HBM peak; "valu-issue" when, below that, the
+    kernel issues VALU on at least VALU_BOUND of its SIMD cycles (valu_util, the
+    third PMC pass: the trace step's branch-free VALU, VERDICT r5 "Next" 2); below
+    both the kernel is bound by
     the latency of its dependent fetch chains -- "hbm-latency" when at least a
     third of that latency is spent on L2 misses (a miss costs ~900 cycles, a hit
     ~200: a gather miss rate above ~10 %, C5's 4.2M-triangle scene beyond the
@@ -419,6 +483,8 @@ def derive_bound(hbm_frac, l2_hit, l2_frac, gather_hit=None):
         return None
     if hbm_frac >= 0.5:
         return "hbm"
+    if valu_util is not None and valu_util >= VALU_BOUND:
+        return "valu-issue"
     hit = gather_hit if gather_hit is not None else l2_hit
     if hit is None:
         return "l2-latency"
@@ -503,7 +569,10 @@ def launch_ranks(args, argv) -> int:
 
 
 def record_exit_code(rc: int) -> None:
-    """A self-launched rank records its exit code for the parent (launch_ranks)."""
+    """A self-launched rank records its exit code for the parent (launch_ranks).  A
+    PMC pass's child (--child) never does: its rank-0 slot belongs to rank 0."""
+    if "--child" in sys.argv[1:]:
+        return
     d = os.environ.get(RC_DIR_ENV)
     if d and os.path.isdir(d):
         with open(os.path.join(d, f"rc.{os.environ.get('RANK', '0')}"), "w") as f:
@@ -538,7 +607,9 @@ def step_rooflines(pmc, excl, ms_per_step):
                   "frac_bounds": [round(lo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                   round(hi / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)],
                   "launches_per_step": round(e["launches_per_step"], 3),
-                  "l2_hit_rate": round(e["l2_hit_rate"], 4) if "l2_hit_rate" in e else None}
+                  "l2_hit_rate": round(e["l2_hit_rate"], 4) if "l2_hit_rate" in e else None,
+                  "valu_util": round(e["valu_util"], 4) if "valu_util" in e else None,
+                  "ta_busy": round(e["ta_busy"], 4) if "ta_busy" in e else None}
     return step, (per or None)
 
 
@@ -747,6 +818,7 @@ def main(argv=None):
             ref_bytes = round(per * samples_per_step / launches_per_step)
 
         traffic = l2hit = ghit = None
+        issue = {}
         traffic_src = None
         step_traffic = None
         census = stored_keyed("census.json", cfg.name, src_hash) if args.kernel == "v3" else None
@@ -755,6 +827,8 @@ def main(argv=None):
         if pmc and kname in pmc:
             e = pmc[kname]
             l2hit = e.get("l2_hit_rate")
+            issue = {k: round(e[k], 4) for k in ("valu_util", "ta_busy", "valu_per_wave", "salu_per_wave", "wait_frac")
+                     if k in e}
             traffic_bounds = [round(GATHER_FACTOR * e["fetch_bytes"] + e["write_bytes"]),
                               round(STREAM_FACTOR * e["fetch_bytes"] + e["write_bytes"])]
             if census and args.kernel == "v3":
@@ -780,7 +854,7 @@ def main(argv=None):
             step_traffic["total_bytes_per_step"] = round(sum(e["bytes_per_launch"] * e["launches_per_step"]
                                                              for e in pmc.values()))
         else:
-            # no live PMC here (N > 1: the passes run at N = 1 only): the N = 1 live
+            # no live PMC (--no-pmc, rocprofv3 absent or a pass failed): the N = 1 live
             # figure recorded for these sources (tools/record_pmc.py), scaled to this
             # rank's launch -- its share of the rows and its frames per launch
             e = stored_keyed("pmc.json", f"{cfg.name}/{kname}", src_hash)
@@ -830,12 +904,17 @@ def main(argv=None):
                                      "MIS / emission term) are not traced; every timed image is checked against the "
                                      "oracle, which traces them all (DESIGN.md section 16)")},
             "roofline": {"bound": derive_bound(achieved / HBM_PEAK_GBS if achieved else None, l2hit,
-                                               requested["frac_of_l2"] if requested else None, ghit),
+                                               requested["frac_of_l2"] if requested else None, ghit,
+                                               issue.get("valu_util")),
                          "bound_rule": "derived from the counters (bench.derive_bound): hbm (bandwidth) if frac >= 0.5; "
-                                       "else the latency of dependent fetch chains -- hbm-latency if L2 misses of the "
+                                       f"else valu-issue if valu_util >= {VALU_BOUND} (SQ_INSTS_VALU x 2 cycles over the "
+                                       "SIMDs' GRBM_GUI_ACTIVE cycles, live third PMC pass); else the latency of "
+                                       "dependent fetch chains -- hbm-latency if L2 misses of the "
                                        "node / triangle gathers (gather_l2_hit_rate; l2_hit_rate when unknown) take "
                                        ">= 1/3 of the fetch latency (miss ~900, hit ~200 cycles), l2-latency otherwise; "
                                        "peak / frac stay against HBM",
+                         "valu_util": issue.get("valu_util"), "ta_busy": issue.get("ta_busy"),
+                         "issue": issue or None,
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -849,6 +928,11 @@ def main(argv=None):
                          "checks": checks,
                          "requested": requested,
                          "reference_bytes_per_launch": ref_bytes,
+                         "reference_bytes_note": ("SURVEY 8d's reference-literal count (no z-cull, no reuse, every record "
+                                                  "access counted): a workload size, never divided by a peak -- over "
+                                                  "kernel_ms it exceeds the HBM peak on the L2-resident scenes (C2: "
+                                                  "~3x), since the tree and triangles are served from L2 (gather L2 "
+                                                  "hit ~0.98); frac above is the counter-measured fabric traffic"),
                          "step": step_roof,
                          "kernels": kernel_roofs},
             "kernels": kernels,

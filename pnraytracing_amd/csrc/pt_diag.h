@@ -62,7 +62,11 @@
 #ifndef WF_DIAG_COOPSTAT
 #define WF_DIAG_COOPSTAT 0
 #endif
-#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS || WF_DIAG_COOP || WF_DIAG_COOPSTAT)
+#if WF_DIAG_COOP_SMALL && !WF_DIAG_COOP
+#error "WF_DIAG_COOP_SMALL shrinks the product finishes' limits: only with WF_DIAG_COOP"
+#endif
+#define PNRT_IS_DIAG_BUILD (WF_STATS || WF_TIMING || WF_DIAG_GUARD || WF_DIAG_BOUNDS || WF_DIAG_COOP || \
+                            WF_DIAG_COOP_SMALL || WF_DIAG_COOPSTAT)
 
 // Fault words (the context's host-mapped fault area, see pt_wf.h wf_fault)
 #define WF_FAULT_GUARD 0     // a bounded wait of the block-level ray queue ran out (diagnostic builds)

@@ -104,6 +104,8 @@ def test_gpus_n_with_nccl_and_too_few_gpus_prints_no_line():
     under --gpus N; and a WORLD_SIZE that disagrees with --gpus is refused."""
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    # no GPU visible to the child on any host: the refusal path, never a real 8-rank launch
+    env.update(HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "1"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "{" not in r.stdout and "needs one GPU per rank" in r.stderr, r.stderr[-2000:]
@@ -127,3 +129,41 @@ def test_step_rooflines():
     assert abs(per["shade"]["frac"] - 0.5) < 1e-9 and per["shade"]["frac_bounds"][0] == round(4.2e9 / 2e-3 / 1e9 / 8000, 4)
     assert per["trace"]["l2_hit_rate"] == 0.8 and per["shade"]["l2_hit_rate"] is None
     assert b.step_rooflines(None, excl, 5.0) == (None, None)
+
+
+def test_pmc_child_runs_the_timed_call_size():
+    """at N > 1 rank 0's PMC child renders its share in calls of the size
+    the timed run issues (32 frames at N = 2, 64 at N >= 4), passed explicitly, with
+    2 calls timed after 1 of warm-up -- so bytes per launch and launches per step
+    are those of the timed launches."""
+    b = _bench()
+    for n, ipc in ((1, 4), (2, 8), (4, 16), (8, 16)):
+        a = b.parse(["--gpus", str(n)])
+        cmd = b.pmc_child_cmd(a, n, "rocprofv3", ("FETCH_SIZE",), "/tmp/x")
+        i = cmd.index("--child")
+        child = cmd[i:]
+        assert child[child.index("--iters-per-call") + 1] == str(ipc), (n, child)
+        assert child[child.index("--steps") + 1] == str(2 * ipc) and child[child.index("--warmup") + 1] == str(ipc)
+        assert child[child.index("--shard-world") + 1] == str(n)
+        # the timed run's own call size for rank 0's share (ShardedFrame.max_rows x W)
+        from pnraytracing_amd.tracer import shard_rows
+        rows = max(len(shard_rows(1080, b.BAND, n, r)) for r in range(n))
+        assert b.iters_per_call(a, rows * 1920) == ipc
+    assert b.pmc_iters_per_call(b.parse(["--config", "C5"]), 1) == 2
+    assert b.pmc_iters_per_call(b.parse(["--config", "D2"]), 1) == 1
+    assert b.pmc_iters_per_call(b.parse(["--iters-per-call", "3"]), 4) == 3
+
+
+def test_issue_stats_and_valu_bound():
+    """The third PMC pass's issue figures (VERDICT r5 "Next" 2): round 5's recorded
+    trace counters (profiles/r05/s23/pmc_valu.txt) give VALU issue 0.65, and the
+    bound reads valu-issue at >= 0.6, the latency classes below it."""
+    b = _bench()
+    st = b.issue_stats({"GRBM_GUI_ACTIVE": 3.154e7, "SQ_INSTS_VALU": 1.312e9, "SQ_WAVES": 8192.0,
+                        "SQ_INSTS_SALU": 5.684e8, "SQ_WAVE_CYCLES": 7.744e9, "SQ_WAIT_ANY": 3.752e9})
+    assert abs(st["valu_util"] - 0.65) < 0.005 and abs(st["valu_per_wave"] - 160156.25) < 1e-6
+    assert abs(st["wait_frac"] - 0.4845) < 1e-3 and "ta_busy" not in st
+    assert b.derive_bound(0.15, 0.8, 0.4, 0.98, 0.65) == "valu-issue"
+    assert b.derive_bound(0.15, 0.8, 0.4, 0.98, 0.5) == "l2-latency"
+    assert b.derive_bound(0.6, 0.8, 0.4, 0.98, 0.7) == "hbm"
+    assert b.derive_bound(0.27, 0.5, 0.4, 0.87, None) == "hbm-latency"
