@@ -272,6 +272,15 @@ PN_DEV LightFetch light_fetch(const DevScene& s, int entry) {
 #ifndef WF_MOOT_TSUM
 #define WF_MOOT_TSUM 1        // the moot test's bound: T_U + T_E (1), or the numerator over the larger reciprocal (0)
 #endif
+#ifndef WF_MOOT_LDS
+#define WF_MOOT_LDS 1         // the moot test reads the light / env candidates back from the lane's LDS slot
+#endif                        // (0: from the P3 / P4 lines it just stored -- an L2 round trip)
+// The lane's LDS copy of its light and env candidates (LDirect, lightPDF; LEnvironment)
+// for the moot test: written where P3 / P4 are stored, read by the same lane.
+PN_DEV float4* wf_moot_lds() {
+    __shared__ float4 c[2 * 256];
+    return c;
+}
 
 // The light record is always fetched with the material.  ENV_EARLY: the env
 // table taps too (gen; in the shade kernel's setup they cost spills, -1.5 %).
@@ -347,6 +356,8 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     // shade takes (0, 0) for a path without a light ray, as the reference's
     // initial LDirect / lightPDF (:878-879)
     if (nfl & WF_RLIGHT) ps_st(w.P3, i, make_float4(LD.x, LD.y, LD.z, pl));
+    if (WF_SKIP_MOOT && WF_MOOT_LDS && MOOT)
+        wf_moot_lds()[threadIdx.x] = (nfl & WF_RLIGHT) ? make_float4(LD.x, LD.y, LD.z, pl) : make_float4(0.f, 0.f, 0.f, 0.f);
     // environment (:911-926)
     f3 LE = mk3(0.f, 0.f, 0.f);
     float pe = 0.f;
@@ -363,6 +374,8 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         }
     }
     if (nfl & WF_RENV) ps_st(w.P4, i, make_float4(LE.x, LE.y, LE.z, 0.f));
+    if (WF_SKIP_MOOT && WF_MOOT_LDS && MOOT)
+        wf_moot_lds()[256 + threadIdx.x] = (nfl & WF_RENV) ? make_float4(LE.x, LE.y, LE.z, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
     // BRDF sample (:928-934) with Cranley-Patterson-rotated Sobol (:539-557)
     uint32_t pseed = ((uint32_t)(x * fp.width) * 1973u + (uint32_t)(py * fp.height) * 9277u +
                       (uint32_t)(114514 / 1919) * 26699u) | 1u;
@@ -455,12 +468,18 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
         // a real value, |N.L| >= 0), which the shade reads as "write Lo1".
         const bool last = bounce + 1 == fp.max_depth;
         if ((nfl & (WF_RLIGHT | WF_RENV)) || last) {
-            // the candidates read back from what P3 / P4 just got (same lane, same
-            // addresses: in order) -- held in registers through the BRDF sample they
-            // cost the kernel two spills
+            // the candidates read back from the lane's own LDS slot (or from what P3 / P4
+            // just got: same lane, same addresses, in order -- an L2 round trip); held in
+            // registers through the BRDF sample they cost the kernel two spills
             asm volatile("" ::: "memory");
-            const float4 r3 = (nfl & WF_RLIGHT) ? w.P3[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 r4 = (nfl & WF_RENV) ? w.P4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 r3, r4;
+            if constexpr (WF_MOOT_LDS) {
+                r3 = wf_moot_lds()[threadIdx.x];
+                r4 = wf_moot_lds()[256 + threadIdx.x];
+            } else {
+                r3 = (nfl & WF_RLIGHT) ? w.P3[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                r4 = (nfl & WF_RENV) ? w.P4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             const f3 acw = mk3(fabsf(q.cw.x), fabsf(q.cw.y), fabsf(q.cw.z));
             const f3 mE = mk3(fabsf(r4.x) * fabsf(pe), fabsf(r4.y) * fabsf(pe), fabsf(r4.z) * fabsf(pe));
             const f3 mU = add(mE, mk3(fabsf(r3.x) * fabsf(r3.w), fabsf(r3.y) * fabsf(r3.w), fabsf(r3.z) * fabsf(r3.w)));
@@ -1249,6 +1268,9 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
     return res;
 }
 
+#ifndef WF_ENV_FAR_FIRST
+#define WF_ENV_FAR_FIRST 1    // env shadow rays traverse far child first (wf_load_ray)
+#endif
 // Ray record `slot` of a kind-`kind` segment -> lane ray state.
 PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode, RayP& r, float& tmax, bool& any,
                         uint32_t& p) {
@@ -1264,6 +1286,13 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
     tmax = kind == 0 ? 1.0f - PT_SHADOW_EPS : PT_FLOAT_MAX;
     any = kind != 2;
     r = make_ray(mk3(ro.x, ro.y, ro.z), mk3(rd.x, rd.y, rd.z), mode);
+    // env shadow rays visit the FAR child first (the sign bits of the near-child
+    // rule inverted): an any-hit ray's result is the OR over every reachable
+    // triangle at its fixed tMax (:464-494; z-culling against a fixed tMax is
+    // order-free too), so any visit order gives the same boolean, and an occluded
+    // env ray leaving a closed room meets its wall sooner from the far side
+    // (tools/step_model: env-ray lane steps -26 % on C2, -28 % on C3)
+    if (WF_ENV_FAR_FIRST && kind == 1) r.perm ^= 0x70;
 }
 
 // Persistent traversal of every queued ray of the bounce.
