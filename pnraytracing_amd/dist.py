@@ -39,12 +39,16 @@ class ShardedFrame:
         self.collective = collective and dist.is_initialized()
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.gworld = self.world          # ranks of the collective (the split's ranks but below)
         if shard is not None:
             # (world, rank) of a split rendered WITHOUT a process group: one rank's share
             # alone (bench.py's PMC pass of rank 0's share); no gather, render() and
-            # pack_rows() use the given split
-            if dist.is_initialized():
-                raise ValueError("ShardedFrame: shard= is for a process without a process group")
+            # pack_rows() use the given split.  With a ONE-rank group and collective=True:
+            # rank 0's share of the split gathered through that group (its side of the
+            # gather, every call's pack + dist.gather + assembly; tools/share_bench.py)
+            if dist.is_initialized() and not (self.collective and self.world == 1 and int(shard[1]) == 0):
+                raise ValueError("ShardedFrame: shard= is for a process without a process group "
+                                 "(or rank 0 of a split over a one-rank group with collective=True)")
             self.world, self.rank = int(shard[0]), int(shard[1])
             if not (self.world >= 1 and 0 <= self.rank < self.world):
                 raise ValueError(f"ShardedFrame: bad shard {shard}")
@@ -81,7 +85,7 @@ class ShardedFrame:
         # renders (gather_async / finish)
         cdev = torch.device("cpu") if self.stage else self.device
         self.sendb = [torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=self.device) for _ in range(2)]
-        self.recvb = [[torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=cdev) for _ in range(self.world)]
+        self.recvb = [[torch.zeros((self.max_rows, W, 4), dtype=torch.float32, device=cdev) for _ in range(self.gworld)]
                       if self.rank == 0 else None for _ in range(2)]
         self.send, self.recv = self.sendb[0], self.recvb[0]
         self._slot = 0
@@ -130,7 +134,7 @@ class ShardedFrame:
         return self._on_stream(self._finish)
 
     def _assemble(self, recv) -> torch.Tensor:
-        for r in range(self.world):
+        for r in range(len(recv)):
             n = len(self.rows[r])
             if n:
                 self.image.index_copy_(0, self.rows[r], recv[r][:n].to(self.device, non_blocking=False))

@@ -131,3 +131,47 @@ def test_single_rank_without_process_group():
     sf.render(0, 1)
     img = sf.gather()
     assert img.shape == (12, 16, 4) and np.array_equal(img.numpy(), tr.accum)
+
+
+def _share_worker(rank, world, port, w, h, band, split, frames, out_path):
+    """Rank 0's share of a `split`-way frame gathered through a ONE-rank group
+    (tools/share_bench.py --collective): bench.py's render / gather_async / finish."""
+    sys.path.insert(0, REPO); sys.path.insert(0, os.path.join(REPO, "oracle")); sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_tracer import OracleTracer
+    from pnraytracing_amd import scenes as S
+    from pnraytracing_amd.dist import ShardedFrame
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        tr = OracleTracer(S.cornell_c1(w, h))
+        with pytest.raises(ValueError):        # a split's share needs collective=True over a one-rank group
+            ShardedFrame(tr, band=band, device="cpu", shard=(split, 0))
+        sf = ShardedFrame(tr, band=band, device="cpu", collective=True, shard=(split, 0))
+        assert sf.world == split and sf.rank == 0 and sf.gworld == 1
+        for f0, n in frames:
+            sf.render(f0, n)
+            sf.gather_async()
+        np.save(out_path, sf.finish().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_share_gathered_through_one_rank_group(tmp_path):
+    """VERDICT r5 "Next" 6: rank 0's share of a 3-way split, gathered through a
+    one-rank group, assembles exactly rank 0's rows of the full render (the other
+    rows stay zero) -- the path tools/share_bench.py --collective times."""
+    import pyoracle
+    from pnraytracing_amd import scenes as S
+    from pnraytracing_amd.dist import row_owner
+    w, h, band, split = 24, 20, 4, 3
+    frames = [(0, 1), (1, 2)]
+    out = str(tmp_path / "img.npy")
+    mp.start_processes(_share_worker, args=(1, _free_port(), w, h, band, split, frames, out), nprocs=1, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    o = pyoracle.Oracle(S.cornell_c1(w, h))
+    ref = np.zeros((h, w, 4), np.float32)
+    for f0, n in frames:
+        o.render(f0, n, accum=ref)
+    mine = row_owner(h, band, split) == 0
+    assert np.array_equal(got[mine].view(np.uint32), ref[mine].view(np.uint32))
+    assert not got[~mine].any()

@@ -1,10 +1,21 @@
 """Rank 0's share of an N-GPU C2 bench run, timed the way bench.py times it:
 one untimed sizing call, a reset, the warm-up calls, a synchronise, then the K
 timed steps as calls of `ipc` 4-spp iterations (the last one cut) and a
-synchronise -- without the gather.  Measures what the calls' size does to a
-rank's rate inside the driver's 20-step region (iters_per_call).
+synchronise.  Measures what the calls' size does to a rank's rate inside the
+driver's 20-step region (iters_per_call).
 
-    python tools/share_bench.py N ipc [steps] [warmup]      (on the GPU box)
+Two columns (VERDICT r5 "Next" 6):
+  plain       the share's calls alone, no gather;
+  collective  the same calls through bench.py's own gather path: a ONE-rank RCCL
+              process group and ShardedFrame(collective=True, shard=(N, 0)) --
+              after every call pack_rows + an asynchronous dist.gather on the
+              double-buffered slots, the last one completed (and the image
+              assembled) inside the timed region, exactly as bench.py's ranks do.
+              What one GPU cannot show is the other N - 1 ranks' rows arriving
+              over xGMI (rank 0 receives (N - 1) / N of the frame per call); the
+              caller reports that transfer's time at the link rate beside it.
+
+    python tools/share_bench.py N ipc [steps] [warmup] [--collective]     (on the GPU box)
 """
 import os
 import sys
@@ -15,30 +26,73 @@ sys.path.insert(0, REPO)
 from pnraytracing_amd import scenes  # noqa: E402
 from pnraytracing_amd.tracer import PathTracer, shard_rows  # noqa: E402
 
-n, ipc = int(sys.argv[1]), int(sys.argv[2])
-steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
-warm = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+collective = "--collective" in sys.argv
+n, ipc = int(argv[0]), int(argv[1])
+steps = int(argv[2]) if len(argv) > 2 else 20
+warm = int(argv[3]) if len(argv) > 3 else 5
 SPP = 4
 cfg = scenes.bunny_c2()
 rows = len(shard_rows(cfg.height, 8, n, 0))
 
 
-def calls(pt, lo, hi):
-    for k in range(lo, hi, ipc):
-        m = min(ipc, hi - k)
-        pt.render(SPP * k, SPP * m, 8, n, 0)
+def groups(lo, hi):
+    return [(k, min(ipc, hi - k)) for k in range(lo, hi, ipc)]
 
 
-with PathTracer(0) as pt:
+if not collective:
+    with PathTracer(0) as pt:
+        pt.load(cfg)
+        pt.render(0, SPP * ipc, 8, n, 0)        # sizing call
+        pt.synchronize()
+        pt.reset_accum()
+        for k, m in groups(0, warm):
+            pt.render(SPP * k, SPP * m, 8, n, 0)
+        pt.synchronize()
+        t = time.perf_counter()
+        for k, m in groups(warm, warm + steps):
+            pt.render(SPP * k, SPP * m, 8, n, 0)
+        pt.synchronize()
+        dt = (time.perf_counter() - t) / steps
+else:
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    from pnraytracing_amd.dist import ShardedFrame
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    pt = PathTracer(0)
+    stream = torch.cuda.ExternalStream(pt.stream_handle())      # as bench.py: torch on the library's stream
+    torch.cuda.set_stream(stream)
+    pt.set_stream(stream.cuda_stream)
     pt.load(cfg)
-    pt.render(0, SPP * ipc, 8, n, 0)        # sizing call
-    pt.synchronize()
+    sf = ShardedFrame(pt, band=8, device=torch.device("cuda", 0), collective=True, shard=(n, 0))
+    sf.render(0, SPP * ipc)                      # sizing call
+    torch.cuda.synchronize()
     pt.reset_accum()
-    calls(pt, 0, warm)
-    pt.synchronize()
+    for k, m in groups(0, warm):
+        sf.render(SPP * k, SPP * m)
+        sf.gather_async()
+    sf.finish()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
     t = time.perf_counter()
-    calls(pt, warm, warm + steps)
-    pt.synchronize()
+    for k, m in groups(warm, warm + steps):
+        sf.render(SPP * k, SPP * m)
+        sf.gather_async()
+    sf.finish()                                  # every gather completes inside the timed region
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / steps
-    per_rank = rows * cfg.width * SPP / dt / 1e6
-    print(f"N={n} ipc={ipc}: rank-0 rows {rows}, {dt * 1e3:.3f} ms/step, {per_rank:.1f} Msamples/s per rank", flush=True)
+    pt.close()
+    dist.destroy_process_group()
+per_rank = rows * cfg.width * SPP / dt / 1e6
+print(f"N={n} ipc={ipc} {'collective' if collective else 'plain'}: rank-0 rows {rows}, {dt * 1e3:.3f} ms/step, "
+      f"{per_rank:.1f} Msamples/s per rank", flush=True)
