@@ -142,6 +142,7 @@ struct pnrt_ctx {
     uint64_t ncall = 0;
     unsigned next_pipe = 0;
     int trace_grid = 0;
+    int trace_grid_cc = 0;     // full occupancy of the lone calls' trace instantiation (WF_TRACE_WAVES_CC)
     int wf_stack_need = 0;                 // wide-traversal stack entries per lane (from upload)
     // per-kernel-class HIP event timing (pnrt_profile_enable / pnrt_profile_read)
     bool prof_on = false;
@@ -358,9 +359,10 @@ static WfLayout wf_layout(char* base, size_t n) {
 // other call is in flight (`alone`: an interactive loop that waits for every
 // frame, the reference's own 512x512 one-frame dispatch) has the chip to itself:
 // full occupancy, one block per WF_TRACE_PATHS_PER_BLOCK_ALONE paths.
-static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false, bool one = false) {
+static unsigned trace_grid_for(const pnrt_ctx* c, size_t n, bool alone = false, bool one = false, bool cc = false) {
     const unsigned pct = (c->serial || alone) ? 100u : one ? WF_TRACE_GRID_PCT_ONE : n < (size_t)WF_SMALL_CALL_PATHS ? WF_TRACE_GRID_PCT : WF_TRACE_GRID_PCT_LARGE;
-    const size_t gmax = (size_t)c->trace_grid * pct / 100;
+    // (cc: the lone calls' instantiation, resident at its own occupancy -- no block waits for a slot)
+    const size_t gmax = (size_t)(cc && c->trace_grid_cc > 0 ? c->trace_grid_cc : c->trace_grid) * pct / 100;
     const size_t ppb = alone ? WF_TRACE_PATHS_PER_BLOCK_ALONE : WF_TRACE_PATHS_PER_BLOCK;
     return ppb ? (unsigned)std::min<size_t>(gmax, std::max<size_t>(64, (n + ppb - 1) / ppb)) : (unsigned)gmax;
 }
@@ -452,7 +454,7 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
         hipLaunchKernelGGL(pt_wf_gen_setup, g, dim3(256), 0, st, s, fp, b, primary, colors);
     }
     HIPCHK(c, hipGetLastError());
-    const unsigned tg = trace_grid_for(c, b.n, alone, one);
+    const unsigned tg = trace_grid_for(c, b.n, alone, one, cc && !s.has_leaf_table);
     // (launch position 2 b: bounce b's trace, 2 b + 1: its shade)
     const int stage_at = std::max(2 * fp.max_depth - WF_STAGGER, 0);
     for (int bounce = 0; bounce < fp.max_depth; ++bounce) {
@@ -557,6 +559,9 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
         HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pt_wf_trace<WF_STACK, false>, WF_TRACE_BLOCK, 0));
         HIPCHK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         c->trace_grid = (per_cu > 0 ? per_cu : 1) * cus;
+        int per_cu_cc = 0;
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_cc, pt_wf_trace<WF_STACK, false, true>, WF_TRACE_BLOCK, 0));
+        c->trace_grid_cc = std::min(c->trace_grid, (per_cu_cc > 0 ? per_cu_cc : 1) * cus);
     }
     // per-lane spill area of the trace kernel's stack: LDS holds WF_STACK entries
     const int ovf_stride = c->wf_stack_need > WF_STACK ? c->wf_stack_need - WF_STACK : 1;

@@ -1087,26 +1087,31 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
     // every read before any write (the owners' stack slots lie in the rows the frontier
     // overwrites).  (Two items per lane, up to 128: the added registers spilled in the
     // lone-call kernel's step loop.)
-    uint32_t o_of[WF_COOP_MAXRAYS], base_of[WF_COOP_MAXRAYS];
+    // ray q's items start at lane base_q (base_0 = 0, base_{q+1} = base_q + sp_q + 2: distinct
+    // positions below 64) -- kept as one 64-bit mask of the bases, and ray q's owner lane in
+    // lane q of `olist`: no per-ray arrays (indexed by a lane's ray they went to scratch)
+    uint64_t bases = 0;
+    uint32_t olist = 0;
     {
         uint64_t m = owners;
         uint32_t base = 0;
 #pragma unroll
         for (int r = 0; r < WF_COOP_MAXRAYS; ++r) {
-            const int o = m ? __ffsll((long long)m) - 1 : 0;
-            o_of[r] = (uint32_t)o;
-            base_of[r] = m ? base : 64u;
-            if (m) base += (((uint32_t)__builtin_amdgcn_readlane((int)t.spa, o)) >> WF_SPA_SHIFT) + 2u;
-            m &= m - 1;
+            if (m) {
+                const int o = __ffsll((long long)m) - 1;
+                bases |= 1ull << base;
+                olist = lane == (uint32_t)r ? (uint32_t)o : olist;
+                base += (((uint32_t)__builtin_amdgcn_readlane((int)t.spa, o)) >> WF_SPA_SHIFT) + 2u;
+                m &= m - 1;
+            }
         }
     }
     auto item = [&](uint32_t l, uint2& e, uint64_t& key) -> bool {
-        uint32_t r = 0, o = o_of[0], jb = base_of[0];
-#pragma unroll
-        for (int q = 1; q < WF_COOP_MAXRAYS; ++q) {
-            const bool in = l >= base_of[q];
-            r = in ? (uint32_t)q : r; o = in ? o_of[q] : o; jb = in ? base_of[q] : jb;
-        }
+        // the lane's ray: the bases at or below l (l < 64)
+        const uint64_t below = bases & (~0ull >> (63u - l));
+        const uint32_t r = (uint32_t)__popcll(below) - 1u;
+        const uint32_t jb = 63u - (uint32_t)__clzll((long long)below);
+        const uint32_t o = (uint32_t)__shfl((int)olist, (int)r);
         const uint32_t ospa = (uint32_t)__shfl((int)t.spa, (int)o);
         const uint32_t ocur = (uint32_t)__shfl((int)t.cur, (int)o);
         const uint32_t olt = (uint32_t)__shfl(t.lt, (int)o);
@@ -1114,7 +1119,7 @@ PN_DEV int wf_coop_multi(const DevScene& s, __amdgpu_buffer_rsrc_t geo, const ui
         const uint32_t j = l - jb;
         e = make_uint2(REF_NONE, 0u);
         key = (uint64_t)r << RS;
-        const bool inRange = l >= base_of[0] && j < sp + 2u;
+        const bool inRange = j < sp + 2u;
         if (inRange && j < sp) {
             const uint32_t a = j * WF_SPA_STRIDE + 8u * otl;
             if (j < (uint32_t)STK) {
@@ -1312,6 +1317,10 @@ PN_DEV void wf_load_ray(const WfBufs& b, uint32_t kind, uint32_t slot, int mode,
 #ifndef WF_TRACE_WAVES
 #define WF_TRACE_WAVES 8      // waves per SIMD (64 VGPRs: no SLP packing, one-register stack position)
 #endif
+#ifndef WF_TRACE_WAVES_CC
+#define WF_TRACE_WAVES_CC 6   // ... for the lone calls' instantiation (CC): 80 VGPRs, no scratch (at 8 waves its
+#endif                        // multi-ray finish spilled 12 values, 80 B per lane); a lone call's grid is one block per
+                              // 256 paths (the reference's 512x512 frame: 4 blocks per CU), within 6 waves per SIMD
 // CC: a wave's last rays, closest-hit ones included, get the cooperative finish (wf_coop_multi) -- its own
 // instantiation, launched for a call with nothing else in flight, so the
 // pipelined launches run code without it (C2 -0.9 % with it compiled in)
@@ -1329,7 +1338,7 @@ PN_DEV bool wf_coop_due(const TravState& t) {
            (t.spa >> WF_SPA_SHIFT) + 2u <= 64u;
 }
 template <int STK, bool TBL, bool CC = false>
-__global__ void __launch_bounds__(WF_TRACE_BLOCK, WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
+__global__ void __launch_bounds__(WF_TRACE_BLOCK, CC ? WF_TRACE_WAVES_CC : WF_TRACE_WAVES) pt_wf_trace(DevScene s, WfBufs b, int mode) {
     __shared__ uint2 lds[(STK + 1) * WF_TRACE_BLOCK];     // STK depths + the spare one (wf_push)
     // the cooperative finishes' frontier: the wave's own stack slots (the other lanes
     // are idle then), an area of its own in WF_DIAG_COOP builds (they are not)
