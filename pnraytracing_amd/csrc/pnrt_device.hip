@@ -299,6 +299,9 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 #ifndef WF_STAGGER_PATHS
 #define WF_STAGGER_PATHS 12000000   // (1080p calls of >= 6 frames; a rank's share at N = 2 with 16-frame calls)
 #endif
+#ifndef WF_CC_MAX_PATHS
+#define WF_CC_MAX_PATHS 4000000     // lone calls of fewer paths per batch run the CC trace instantiation (the
+#endif                              // reference's 512x512 frame: 262k); larger ones the pipelined one at 8 waves
 #ifndef WF_ALONE_ON_CALLER
 #define WF_ALONE_ON_CALLER 1        // a call with nothing in flight runs on the caller's stream (no worker hop)
 #endif
@@ -445,7 +448,9 @@ static int render_batch(pnrt_ctx* c, const DevScene& s, const FrameParams& fp, c
     // idle -- a call with nothing else in flight (the reference's loop: D2 sync -19 %);
     // beside other calls' kernels the wave's 64 lanes on one ray cost more than they
     // save (C2 -2.3 %), so pipelined calls run the instantiation without it
-    const bool cc = alone && WF_COOP_TAIL >= 2;
+    // (only for batches below WF_CC_MAX_PATHS: the lone call's instantiation runs at
+    // WF_TRACE_WAVES_CC waves per SIMD, fewer than a large batch's stepping wants)
+    const bool cc = alone && WF_COOP_TAIL >= 2 && (size_t)b.n < (size_t)WF_CC_MAX_PATHS;
     const dim3 g((unsigned)((b.n + 255) / 256));
     b.wr = L.set[0];
     if (WF_STATS) HIPCHK(c, hipMemsetAsync(b.stats + 56, 0, 64, st));    // the setups' moot-ray counts

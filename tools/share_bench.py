@@ -32,6 +32,10 @@ n, ipc = int(argv[0]), int(argv[1])
 steps = int(argv[2]) if len(argv) > 2 else 20
 warm = int(argv[3]) if len(argv) > 3 else 5
 SPP = 4
+if n > 1:
+    # as bench.py's ranks (world > 1): 8 hardware queues, so RCCL's stream gets one beside the
+    # library's four (set before anything initialises HIP)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 cfg = scenes.bunny_c2()
 rows = len(shard_rows(cfg.height, 8, n, 0))
 
@@ -83,14 +87,20 @@ else:
     dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter()
+    marks = []
     for k, m in groups(warm, warm + steps):
         sf.render(SPP * k, SPP * m)
+        marks.append(time.perf_counter() - t)
         sf.gather_async()
+        marks.append(time.perf_counter() - t)
     sf.finish()                                  # every gather completes inside the timed region
+    marks.append(time.perf_counter() - t)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / steps
+    if os.environ.get("SHARE_MARKS"):           # host-side time after each render / gather_async / finish
+        print("marks ms:", " ".join(f"{x * 1e3:.2f}" for x in marks), f"end {dt * steps * 1e3:.2f}", flush=True)
     pt.close()
     dist.destroy_process_group()
 per_rank = rows * cfg.width * SPP / dt / 1e6
