@@ -76,9 +76,13 @@ struct Ray {
     int kz;
     float tmax;
     bool any;
+    bool flip;        // far child first (an any-hit ray's visit order is free): the product flips env rays
 };
-static Ray mkray(V3 o, V3 d, float tmax, bool any) {
-    Ray r{o, d, v3(1.f / d.x, 1.f / d.y, 1.f / d.z), 2, tmax, any};
+static int g_flipmode = 2;        // FLIP: 0 no any-hit ray flipped, 1 every any-hit ray, 2 env rays (the product)
+static int g_anyord = 0;          // ANYORD: any-hit rays by a fixed per-node order -- 1 larger child first, 2 smaller
+static Ray mkray(V3 o, V3 d, float tmax, bool any, bool env = false) {
+    Ray r{o, d, v3(1.f / d.x, 1.f / d.y, 1.f / d.z), 2, tmax, any,
+          any && (g_flipmode == 1 || (g_flipmode == 2 && env))};
     if (d.z == 0.f) r.kz = std::fabs(d.x) > std::fabs(d.y) ? 0 : 1;
     return r;
 }
@@ -125,37 +129,47 @@ static float tri(const Scene& s, const Ray& r, int t, float tmax) {
     return ts * (1.f / det);
 }
 
-struct Entry { int node; float z; };
-static bool g_anyflip = false;
-static int g_anyord = 0;          // any-hit rays: 0 near/far by direction, 1 larger child first, 2 smaller first     // any-hit rays visit the far child first (their result is order-free)   // node index (interior or leaf), z-slab lower end
+struct Entry { int node; float z; };   // node index (interior or leaf), z-slab lower end
+
+// per (ray kind, bounce) census of the device traversal (the C3-vs-C2 record)
+struct Census {
+    double rays = 0, nodes = 0, tris = 0, leaves = 0, leaf_tris = 0, accepted = 0, depth_sum = 0;
+    double depth_hist[6] = {0, 0, 0, 0, 0, 0};    // node visits by depth: 0-3, 4-7, ..., 20+
+};
+static std::vector<int> g_depth;
 
 // The device traversal (binary, one node or one triangle per step): returns the hit
-// triangle (-1), the step kinds ('N' / 'T'), the hit distance
-static int trace_bin(const Scene& s, Ray r, std::string* seq, float* thit, int* leaves = nullptr) {
+// triangle (-1), the step kinds ('N' / 'T'), the hit distance; the census when given
+static int trace_bin(const Scene& s, Ray r, std::string* seq, float* thit, Census* cs = nullptr) {
     float zlo, zhi;
     if (seq) seq->clear();
+    if (cs) cs->rays += 1;
+    auto enter_leaf = [&](int n) { if (cs) { cs->leaves += 1; cs->leaf_tris += s.t1(n) - s.t0(n); } };
     if (!box(r, s.box(0), zlo, zhi)) return -1;
     std::vector<Entry> st;
     int cur = 0, hit = -1;
     int lt = 0, lc = 0;
-    if (s.leaf(0)) { lt = s.t0(0); lc = s.t1(0) - lt; cur = -1; }
+    if (s.leaf(0)) { lt = s.t0(0); lc = s.t1(0) - lt; cur = -1; enter_leaf(0); }
     for (;;) {
         if (lc > 0) {
             if (seq) seq->push_back('T');
+            if (cs) cs->tris += 1;
             float t = tri(s, r, lt, r.tmax);
             if (t >= 0) {
                 hit = lt;
+                if (cs) cs->accepted += 1;
                 if (r.any) return hit;
                 r.tmax = t;
             }
             ++lt; --lc;
         } else if (cur >= 0) {
             if (seq) seq->push_back('N');
+            if (cs) { cs->nodes += 1; cs->depth_sum += g_depth[cur]; cs->depth_hist[std::min(5, g_depth[cur] / 4)] += 1; }
             int L = cur + 1, R = s.right(cur);
             float zl, zr, h;
             bool hl = box(r, s.box(L), zl, h) && !culled(zl, r.tmax);
             bool hr = box(r, s.box(R), zr, h) && !culled(zr, r.tmax);
-            bool rf = (c3(r.d, s.axis(cur)) < 0) != (r.any && g_anyflip);
+            bool rf = (c3(r.d, s.axis(cur)) < 0) != r.flip;
             if (r.any && g_anyord) {     // a fixed per-node preference: the child of larger (1) / smaller (2) surface area
                 auto sa = [&](int c) { const float* b = s.box(c); float dx = b[3] - b[0], dy = b[4] - b[1], dz = b[5] - b[2];
                                        return dx * dy + dy * dz + dz * dx; };
@@ -169,7 +183,7 @@ static int trace_bin(const Scene& s, Ray r, std::string* seq, float* thit, int* 
             if (hn) { if (hf) st.push_back({farc, zf}); go = nearc; }
             else if (hf) go = farc;
             if (go >= 0) {
-                if (s.leaf(go)) { lt = s.t0(go); lc = s.t1(go) - lt; if (leaves) ++*leaves; }
+                if (s.leaf(go)) { lt = s.t0(go); lc = s.t1(go) - lt; enter_leaf(go); }
                 else cur = go;
             }
         }
@@ -179,7 +193,7 @@ static int trace_bin(const Scene& s, Ray r, std::string* seq, float* thit, int* 
                 Entry e = st.back();
                 st.pop_back();
                 if (culled(e.z, r.tmax)) continue;
-                if (s.leaf(e.node)) { lt = s.t0(e.node); lc = s.t1(e.node) - lt; if (leaves) ++*leaves; }
+                if (s.leaf(e.node)) { lt = s.t0(e.node); lc = s.t1(e.node) - lt; enter_leaf(e.node); }
                 else cur = e.node;
                 break;
             }
@@ -210,7 +224,7 @@ static void trace_quad(const Scene& s, Ray r, std::string& seq) {
             // the children in the reference's order, each expanded once more if interior
             std::vector<Entry> order;   // visit order (first = next)
             int L = cur + 1, R = s.right(cur);
-            bool rf = c3(r.d, s.axis(cur)) < 0;
+            bool rf = (c3(r.d, s.axis(cur)) < 0) != r.flip;
             int cs[2] = {rf ? R : L, rf ? L : R};
             for (int c : cs) {
                 float zc, h;
@@ -219,7 +233,7 @@ static void trace_quad(const Scene& s, Ray r, std::string& seq) {
                     continue;
                 }
                 int cl = c + 1, cr = s.right(c);
-                bool crf = c3(r.d, s.axis(c)) < 0;
+                bool crf = (c3(r.d, s.axis(c)) < 0) != r.flip;
                 int gs[2] = {crf ? cr : cl, crf ? cl : cr};
                 for (int g : gs) {
                     float zg;
@@ -336,8 +350,13 @@ int main(int argc, char** argv) {
     V3 eye = v3(s.cam[0], s.cam[1], s.cam[2]), ll = v3(s.cam[3], s.cam[4], s.cam[5]);
     V3 hor = v3(s.cam[6], s.cam[7], s.cam[8]), ver = v3(s.cam[9], s.cam[10], s.cam[11]);
     std::mt19937 rng(7);
-    g_anyflip = getenv("ANYFLIP") && *getenv("ANYFLIP") == '1';
+    if (getenv("FLIP")) g_flipmode = atoi(getenv("FLIP"));
     g_anyord = getenv("ANYORD") ? atoi(getenv("ANYORD")) : 0;
+    // node depths (left child = i + 1, right child = node[7]) for the census
+    g_depth.assign(s.nn, 0);
+    for (int i = 0; i < s.nn; ++i)
+        if (!s.leaf(i)) { g_depth[i + 1] = g_depth[i] + 1; g_depth[s.right(i)] = g_depth[i] + 1; }
+    Census cen[3][4];     // [cont, env, light][bounce]
     std::uniform_real_distribution<float> U(0.f, 1.f);
     auto face_n = [&](int t) {
         const float* p = &s.T[9 * t];
@@ -357,7 +376,6 @@ int main(int argc, char** argv) {
                 }
     printf("paths %zu (every %d-th 8x8 tile of %dx%d, %d frames), nodes %d, triangles %d\n", paths.size(), tstep, Wd, Hd,
            frames, s.nn, s.nt);
-    double tot_iters[5] = {0}, tot_valu[5] = {0}, tot_lanes[5] = {0};
     double sumN = 0, sumT = 0, sumG = 0, sumTq = 0, nrays = 0;
     const int KS[] = {0, 2, 4, 6, 8, 12, 16};
     const int NP = 4 + (int)(sizeof(KS) / sizeof(KS[0]));
@@ -387,7 +405,7 @@ int main(int argc, char** argv) {
             float r1 = U(rng), r2 = U(rng), ph = 6.2831853f * r1, sr = std::sqrt(r2);
             V3 dc = norm(add(add(mul(t, sr * std::cos(ph)), mul(bb, sr * std::sin(ph))), mul(n, std::sqrt(1 - r2))));
             std::string sq;
-            trace_bin(s, mkray(oo, dc, 3.402823466e38f, false), &sq, nullptr);
+            trace_bin(s, mkray(oo, dc, 3.402823466e38f, false), &sq, nullptr, &cen[0][b]);
             qc.push_back(sq);
             std::string sq4;
             trace_quad(s, mkray(oo, dc, 3.402823466e38f, false), sq4);
@@ -401,7 +419,7 @@ int main(int argc, char** argv) {
                 V3 q = add(add(mul(v3(p[0], p[1], p[2]), 1 - a), mul(v3(p[3], p[4], p[5]), a * (1 - c))),
                            mul(v3(p[6], p[7], p[8]), a * c));
                 V3 dl = sub(q, oo);
-                trace_bin(s, mkray(oo, dl, 1.f - 1e-4f, true), &sq, nullptr);
+                trace_bin(s, mkray(oo, dl, 1.f - 1e-4f, true), &sq, nullptr, &cen[2][b]);
                 ql.push_back(sq);
                 trace_quad(s, mkray(oo, dl, 1.f - 1e-4f, true), sq4);
                 qlq.push_back(sq4);
@@ -410,19 +428,13 @@ int main(int argc, char** argv) {
             if (U(rng) < 0.18f) {
                 V3 de = norm(v3(U(rng) * 2 - 1, U(rng) * 2 - 1, U(rng) * 2 - 1));
                 if (dot(de, n) < 0) de = mul(de, -1.f);
-                trace_bin(s, mkray(X, de, 3.402823466e38f, true), &sq, nullptr);
+                trace_bin(s, mkray(X, de, 3.402823466e38f, true, true), &sq, nullptr, &cen[1][b]);
                 qe.push_back(sq);
-                trace_quad(s, mkray(X, de, 3.402823466e38f, true), sq4);
+                trace_quad(s, mkray(X, de, 3.402823466e38f, true, true), sq4);
                 qeq.push_back(sq4);
             }
         }
         if (getenv("PER_KIND")) {
-            for (int fl = 0; fl < 2; ++fl) {
-                g_anyflip = fl == 1;
-                // re-trace this bounce's shadow rays with the flipped order is not stored: report the
-                // stored sequences (traced with the current order) per kind
-            }
-            g_anyflip = getenv("ANYFLIP") && *getenv("ANYFLIP") == '1';
             auto mean = [](const std::vector<std::string>& v, char c) {
                 double n = 0; for (auto& x : v) for (char y : x) n += (c == 'T') == (y == 'T'); return v.empty() ? 0 : n / v.size(); };
             printf("  per kind: cont N %.2f T %.2f | env N %.2f T %.2f | light N %.2f T %.2f\n", mean(qc, 'N'), mean(qc, 'T'),
@@ -466,5 +478,21 @@ int main(int argc, char** argv) {
     }
     printf("\nVALU per iteration kind: unified %.0f, node-only %.0f, triangle-only %.0f, grandchild unified %.0f\n", VU, VN,
            VT, VG);
+    // the census: per ray kind and bounce -- node visits and triangle tests per ray, leaves
+    // entered and their mean size, triangle tests per accepted triangle (closest hit: every
+    // acceptance that shrank tMax; any hit: the occluding one), node-visit depth histogram
+    const char* kn[3] = {"cont", "env", "light"};
+    printf("\ncensus (flip mode %d): kind bounce | rays | nodes/ray tris/ray | leaves/ray mean-leaf-size | tris/accept | "
+           "mean depth | node visits by depth 0-3 4-7 8-11 12-15 16-19 20+ (%%)\n", g_flipmode);
+    for (int k = 0; k < 3; ++k)
+        for (int b = 0; b < depth; ++b) {
+            const Census& c = cen[k][b];
+            if (!c.rays) continue;
+            printf("  %-5s %d | %7.0f | %5.2f %5.2f | %5.2f %5.2f | %6.2f | %5.1f |", kn[k], b, c.rays, c.nodes / c.rays,
+                   c.tris / c.rays, c.leaves / c.rays, c.leaves ? c.leaf_tris / c.leaves : 0, c.accepted ? c.tris / c.accepted : 0,
+                   c.nodes ? c.depth_sum / c.nodes : 0);
+            for (int d = 0; d < 6; ++d) printf(" %4.1f", c.nodes ? 100 * c.depth_hist[d] / c.nodes : 0);
+            printf("\n");
+        }
     return 0;
 }
