@@ -421,6 +421,17 @@ def call_groups(lo: int, hi: int, ipc: int):
     return [(k, min(ipc, hi - k)) for k in range(lo, hi, max(1, ipc))]
 
 
+def sizing_calls(warmup: int, steps: int, ipc: int):
+    """Iterations of the untimed calls issued before the warm-up: one per distinct call
+    size of the warm-up and timed plans, the timed calls' size first.  A call size
+    selects how many buffer sets ("pipes") calls of that size rotate over (by paths per
+    batch), and the first call of a size sizes all of them -- so the cut last call of a
+    plan (e.g. 4 iterations after a 16-iteration call at N = 8) allocates nothing inside
+    the timed region."""
+    sizes = {m for _, m in call_groups(0, warmup, ipc) + call_groups(warmup, warmup + steps, ipc)}
+    return [ipc] + sorted(sizes - {ipc}, reverse=True)
+
+
 def issue_calls(sf, spp: int, lo: int, hi: int, ipc: int, world: int) -> int:
     """The pnrt_render calls of iterations [lo, hi): one per group of ipc
     iterations (the last group cut at hi); multi-GPU ranks start one gather of
@@ -710,7 +721,8 @@ def main(argv=None):
     # warm-up's and timed steps' frames as before), so that no later call -- a shorter
     # warm-up call included -- reallocates inside the warm-up or the timed region
     if not args.child:                         # (a PMC pass's warm-up is whole calls: it sizes them,
-        sf.render(0, spp * ipc)                # and its launch counts stay those of its steps)
+        for m in sizing_calls(args.warmup, args.steps, ipc):   # and its launch counts stay those of its steps)
+            sf.render(0, spp * m)
         torch.cuda.synchronize()
         pt.reset_accum()
     calls(0, args.warmup)

@@ -44,10 +44,17 @@ def groups(lo, hi):
     return [(k, min(ipc, hi - k)) for k in range(lo, hi, ipc)]
 
 
+# untimed sizing calls, as bench.py issues them (bench.sizing_calls): one per distinct call size
+SIZES = [ipc] + sorted({m for _, m in groups(0, warm) + groups(warm, warm + steps)} - {ipc}, reverse=True)
+if os.environ.get("SHARE_ONE_SIZING"):       # (the round-5 plan: the timed calls' size only)
+    SIZES = [ipc]
+
+
 if not collective:
     with PathTracer(0) as pt:
         pt.load(cfg)
-        pt.render(0, SPP * ipc, 8, n, 0)        # sizing call
+        for m in SIZES:                          # sizing calls
+            pt.render(0, SPP * m, 8, n, 0)
         pt.synchronize()
         pt.reset_accum()
         for k, m in groups(0, warm):
@@ -76,7 +83,8 @@ else:
     pt.set_stream(stream.cuda_stream)
     pt.load(cfg)
     sf = ShardedFrame(pt, band=8, device=torch.device("cuda", 0), collective=True, shard=(n, 0))
-    sf.render(0, SPP * ipc)                      # sizing call
+    for m in SIZES:                              # sizing calls
+        sf.render(0, SPP * m)
     torch.cuda.synchronize()
     pt.reset_accum()
     for k, m in groups(0, warm):
