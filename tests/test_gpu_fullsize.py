@@ -7,7 +7,7 @@ properties.
   every Disney lobe): every pixel vs the oracle.
 * C4 (1920x1080, teapot + area light + env: all three pdfs active): every
   pixel vs the oracle.
-* C5 (3840x2160, 4.19M triangles, 4k env): every 16th row vs the oracle.
+* C5 (3840x2160, 4.19M triangles, 4k env): every pixel vs the oracle.
 * C4 / C5: EXACT = ZCULL = v1 kernels on every pixel; the union of the 8
   row-band shards of the 8-GPU split (one pnrt_render call per
   shard as each rank makes it) = the single-call frame, bit for bit.
@@ -89,16 +89,15 @@ def test_c4_whole_frame_bitwise(pt):
     assert_bitwise(got, ref, "C4 1920x1080 whole frame")
 
 
-def test_c5_fullsize_rows_bitwise(pt):
+def test_c5_whole_frame_bitwise(pt):
     """C5 at its full 3840x2160 with the 4.19M-triangle BVH and the 4k env:
-    every 16th row (135 rows x 3840 x 4 spp) vs the oracle."""
+    every pixel (33.2M samples) vs the oracle (it was every 16th
+    row; the oracle takes ~25 s on the box's 16 CPUs)."""
     c = cfg("C5")
     got = gpu_render(pt, c, 0, 4)
-    ref = np.zeros_like(got)
-    _, st = pyoracle.Oracle(c).render(0, 4, rows=(7, c.height), y_step=16, accum=ref)
+    ref, st = pyoracle.Oracle(c).render(0, 4)
     assert st["stack_overflow"] == 0
-    rows = np.arange(7, c.height, 16)
-    assert_bitwise(got[rows], ref[rows], "C5 3840x2160 rows")
+    assert_bitwise(got, ref, "C5 3840x2160 whole frame")
     assert np.isfinite(got).all() and (got[..., 3] == 1).all()
 
 
