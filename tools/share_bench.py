@@ -50,8 +50,44 @@ if os.environ.get("SHARE_ONE_SIZING"):       # (the round-5 plan: the timed call
     SIZES = [ipc]
 
 
+# diagnostic (SHARE_PROBE): the plain calls, but in a process that first initialises torch's HIP context
+# ("torch"), also puts torch on the library's stream ("stream"), or also joins a one-rank RCCL group ("dist")
+probe = os.environ.get("SHARE_PROBE", "")
+if probe and not collective:
+    import torch
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")
+    if probe == "indexcopy":          # one torch index_copy_ (small tensors)
+        torch.zeros((64, 4), device="cuda").index_copy_(0, torch.arange(8, device="cuda"), torch.ones((8, 4), device="cuda"))
+    if probe == "stridedcopy":        # one strided torch copy_ (small tensors)
+        torch.zeros((16, 4), device="cuda")[::2].copy_(torch.ones((8, 4), device="cuda"))
+    if probe == "sort":               # an unrelated torch kernel family
+        torch.sort(torch.rand(1024, device="cuda"))
+    torch.cuda.synchronize()
+    if probe in ("dist", "gather", "allgather", "gatherbig", "gatherasync"):
+        import socket
+        import torch.distributed as dist
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(so.getsockname()[1]), RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+        x = torch.zeros(1024, device="cuda")
+        big = torch.zeros((136, 1920, 4), device="cuda")
+        if probe == "gather":         # one RCCL gather (send / recv to itself) before the calls
+            dist.gather(x, [torch.zeros_like(x)], dst=0)
+        if probe == "gatherbig":      # ... of a rank's 4.2 MB share
+            dist.gather(big, [torch.zeros_like(big)], dst=0)
+        if probe == "gatherasync":    # ... asynchronous, then waited for (ShardedFrame.gather_async / finish)
+            dist.gather(big, [torch.zeros_like(big)], dst=0, async_op=True).wait()
+        if probe == "allgather":      # one RCCL ring collective instead
+            dist.all_gather_into_tensor(torch.zeros_like(x), x)
+        torch.cuda.synchronize()
 if not collective:
     with PathTracer(0) as pt:
+        if probe in ("stream", "dist", "gather", "allgather", "gatherbig", "gatherasync"):
+            stream = torch.cuda.ExternalStream(pt.stream_handle())
+            torch.cuda.set_stream(stream)
+            pt.set_stream(stream.cuda_stream)
         pt.load(cfg)
         for m in SIZES:                          # sizing calls
             pt.render(0, SPP * m, 8, n, 0)
@@ -87,24 +123,47 @@ else:
         sf.render(0, SPP * m)
     torch.cuda.synchronize()
     pt.reset_accum()
+    wg_mode = os.environ.get("SHARE_WARMGATHER", "1")                # (diagnostic switches)
+    warm_gather = wg_mode == "1"
+    barrier = os.environ.get("SHARE_BARRIER", "1") == "1"
+    sync_first = os.environ.get("SHARE_SYNCFIRST") == "1"
     for k, m in groups(0, warm):
         sf.render(SPP * k, SPP * m)
-        sf.gather_async()
-    sf.finish()
+        if sync_first:
+            torch.cuda.synchronize()
+        if warm_gather:
+            sf.gather_async()
+        elif wg_mode == "pack":
+            pt.pack_rows(sf.sendb[0].data_ptr(), 8, n, 0)
+        elif wg_mode == "gatheronly":
+            dist.gather(sf.sendb[0], sf.recvb[0], dst=0, async_op=True).wait()
+        elif wg_mode == "assemble":
+            sf._assemble(sf.recvb[0])
+    if warm_gather:
+        sf.finish()
     torch.cuda.synchronize()
-    dist.barrier()
+    if os.environ.get("SHARE_SLEEP"):
+        time.sleep(float(os.environ["SHARE_SLEEP"]))
+    if barrier:
+        dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter()
     marks = []
+    what = os.environ.get("SHARE_COLL", "gather")    # diagnostic: "render" (no gather), "pack" (pack only)
     for k, m in groups(warm, warm + steps):
         sf.render(SPP * k, SPP * m)
         marks.append(time.perf_counter() - t)
-        sf.gather_async()
+        if what == "gather":
+            sf.gather_async()
+        elif what == "pack":
+            pt.pack_rows(sf.sendb[0].data_ptr(), 8, n, 0)
         marks.append(time.perf_counter() - t)
-    sf.finish()                                  # every gather completes inside the timed region
+    if what == "gather":
+        sf.finish()                              # every gather completes inside the timed region
     marks.append(time.perf_counter() - t)
     torch.cuda.synchronize()
-    dist.barrier()
+    if barrier:
+        dist.barrier()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / steps
     if os.environ.get("SHARE_MARKS"):           # host-side time after each render / gather_async / finish
