@@ -148,6 +148,13 @@ void* pnrt_accum_device_ptr(pnrt_ctx* ctx);
 /* Copy this shard's rows, in increasing y, into a contiguous device buffer
  * (rows_of_shard * width * 4 floats), on the context stream. */
 int pnrt_pack_rows(pnrt_ctx* ctx, void* dst_device, int band_rows, int n_shards, int shard);
+/* The inverse, on the receiving rank of the gather: shard `shard`'s packed rows
+ * (as pnrt_pack_rows wrote them on that rank) into their rows of a
+ * width*height*4-float device image (row 0 = bottom), on the context stream --
+ * the gathered frame assembled by the library's own kernel (the main.cpp
+ * display reads one image, main.cpp:613-628). */
+int pnrt_unpack_rows(pnrt_ctx* ctx, const void* src_device, void* image_device, int band_rows, int n_shards,
+                     int shard);
 int pnrt_synchronize(pnrt_ctx* ctx);
 int pnrt_get_device_info(pnrt_ctx* ctx, pnrt_device_info* info);
 

@@ -140,6 +140,7 @@ def _type_device(lib):
     _sig(lib, "pnrt_read_accum", INT, P, F)
     _sig(lib, "pnrt_accum_device_ptr", P, P)
     _sig(lib, "pnrt_pack_rows", INT, P, P, INT, INT, INT)
+    _sig(lib, "pnrt_unpack_rows", INT, P, P, P, INT, INT, INT)
     _sig(lib, "pnrt_synchronize", INT, P)
     _sig(lib, "pnrt_get_device_info", INT, P, ctypes.POINTER(DeviceInfo))
     _sig(lib, "pnrt_debug_math", INT, P, INT, F, F, F, INT)

@@ -32,6 +32,17 @@ __global__ void pt_pack_rows_kernel(const float4* accum, float4* dst, int width,
     dst[i] = accum[(size_t)y * width + x];
 }
 
+// the inverse of pt_pack_rows_kernel: a shard's packed rows into their image rows
+__global__ void pt_unpack_rows_kernel(const float4* src, float4* img, int width, int rows, int band, int n_shards,
+                                      int shard) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t total = (size_t)rows * width;
+    if (i >= total) return;
+    int r = (int)(i / width), x = (int)(i - (size_t)r * width);
+    int y = shard_row(r, band, n_shards, shard);
+    img[(size_t)y * width + x] = src[i];
+}
+
 __global__ void pt_math_kernel(int fn, const float* a, const float* b, float* out, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1320,6 +1331,20 @@ int pnrt_pack_rows(pnrt_ctx* c, void* dst, int band, int nsh, int shard) {
     if (total == 0) return PNRT_OK;
     hipLaunchKernelGGL(pt_pack_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream,
                        c->accum, static_cast<float4*>(dst), c->width, rows, band, nsh, shard);
+    HIPCHK(c, hipGetLastError());
+    return mark_stream(c);
+}
+
+int pnrt_unpack_rows(pnrt_ctx* c, const void* src, void* image, int band, int nsh, int shard) {
+    if (!c || !src || !image) return PNRT_E_ARG;
+    if (c->width <= 0 || c->height <= 0) return set_err(c, PNRT_E_STATE, "unpack_rows: no frame");
+    if (band < 1 || nsh < 1 || shard < 0 || shard >= nsh) return set_err(c, PNRT_E_ARG, "unpack_rows: bad shard selector");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rows = shard_rows(c->height, band, nsh, shard);
+    size_t total = (size_t)rows * c->width;
+    if (total == 0) return PNRT_OK;
+    hipLaunchKernelGGL(pt_unpack_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, c->stream,
+                       static_cast<const float4*>(src), static_cast<float4*>(image), c->width, rows, band, nsh, shard);
     HIPCHK(c, hipGetLastError());
     return mark_stream(c);
 }

@@ -134,9 +134,18 @@ class ShardedFrame:
         return self._on_stream(self._finish)
 
     def _assemble(self, recv) -> torch.Tensor:
+        # device images from a tracer that can unpack: the library's own kernel on its stream
+        # (torch's index_copy_ there left the library's later kernels 5-10 % slower on the
+        # one-GPU box, tools/share_bench.py -- DESIGN.md section 17)
+        lib = (self.device.type == "cuda" and hasattr(self.tracer, "unpack_rows") and
+               all(t.device == self.device for t in recv))
         for r in range(len(recv)):
             n = len(self.rows[r])
-            if n:
+            if not n:
+                continue
+            if lib:
+                self.tracer.unpack_rows(recv[r].data_ptr(), self.image.data_ptr(), self.band, self.world, r)
+            else:
                 self.image.index_copy_(0, self.rows[r], recv[r][:n].to(self.device, non_blocking=False))
         return self.image
 

@@ -151,6 +151,12 @@ class PathTracer:
     def pack_rows(self, dst_ptr: int, band: int, n_shards: int, shard: int):
         self._ck(self._lib.pnrt_pack_rows(self._ctx, ctypes.c_void_p(dst_ptr), band, n_shards, shard), "pnrt_pack_rows")
 
+    def unpack_rows(self, src_ptr: int, dst_ptr: int, band: int, n_shards: int, shard: int):
+        """Shard `shard`'s packed rows (device buffer) into their rows of a device image
+        (height x width x 4 floats), on the context stream (pnrt_unpack_rows)."""
+        self._ck(self._lib.pnrt_unpack_rows(self._ctx, ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr), band,
+                                            n_shards, shard), "pnrt_unpack_rows")
+
     def device_info(self) -> dict:
         info = N.DeviceInfo()
         self._ck(self._lib.pnrt_get_device_info(self._ctx, ctypes.byref(info)), "pnrt_get_device_info")

@@ -10,6 +10,7 @@
 //     pnrt_render(ctx, f, n, 8, N, r)                  rows y with (y / 8) % N == r
 //     pnrt_pack_rows(ctx, send + slot, 8, N, r)        contiguous rows, padded to max_rows
 //   ncclGroupStart; ncclGather(send_d -> recv on device 0) per device; ncclGroupEnd
+//   pnrt_unpack_rows(ctx[0], recv + slot of shard r, image, 8, N, r)   every shard's rows into one image
 //   device 0: rows scattered back into image order
 //
 // and checks the gathered image against one single-context render of the whole
@@ -153,15 +154,18 @@ int main(int argc, char** argv) {
         if (pnrt_synchronize(ctx[r])) { fprintf(stderr, "shard %d: %s\n", r, pnrt_last_error(ctx[r])); return 8; }
 
     // device 0: de-interleave (recv = device-major, slot-minor: shard r at d * per_dev + r / ndev)
-    std::vector<float> g(slot * per_dev * ndev), img((size_t)W * H * 4, 0.f);
+    // into a device image with the library's pnrt_unpack_rows, on shard 0's context (device 0)
+    std::vector<float> img((size_t)W * H * 4, 0.f);
     HIPCK(hipSetDevice(0));
-    HIPCK(hipMemcpy(g.data(), recv, g.size() * sizeof(float), hipMemcpyDeviceToHost));
-    for (int r = 0; r < N; ++r) {
-        const float* src = g.data() + slot * ((size_t)(r % ndev) * per_dev + r / ndev);
-        int k = 0;
-        for (int y = 0; y < H; ++y)
-            if ((y / BAND) % N == r) memcpy(&img[(size_t)y * W * 4], src + (size_t)(k++) * W * 4, (size_t)W * 16);
-    }
+    float* dimg = nullptr;
+    HIPCK(hipMalloc(&dimg, img.size() * sizeof(float)));
+    HIPCK(hipMemset(dimg, 0, img.size() * sizeof(float)));
+    for (int r = 0; r < N; ++r)
+        CK("unpack_rows", pnrt_unpack_rows(ctx[0], recv + slot * ((size_t)(r % ndev) * per_dev + r / ndev), dimg, BAND,
+                                           N, r));
+    CK("synchronize (unpack)", pnrt_synchronize(ctx[0]));
+    HIPCK(hipMemcpy(img.data(), dimg, img.size() * sizeof(float), hipMemcpyDeviceToHost));
+    (void)hipFree(dimg);
 
     // the single-context render of the whole frame
     pnrt_ctx* one = nullptr;

@@ -139,6 +139,15 @@ else:
             dist.gather(sf.sendb[0], sf.recvb[0], dst=0, async_op=True).wait()
         elif wg_mode == "assemble":
             sf._assemble(sf.recvb[0])
+        elif wg_mode == "fillimg":        # a torch kernel on the library's stream, on the image
+            sf.image.fill_(0.0)
+        elif wg_mode == "fillsmall":      # a torch kernel on the library's stream, small
+            torch.zeros(64, device="cuda").fill_(1.0)
+        elif wg_mode == "assembledef":    # the assembly on torch's default stream
+            torch.cuda.synchronize()
+            with torch.cuda.stream(torch.cuda.default_stream()):
+                sf.image.index_copy_(0, sf.rows[0], sf.recvb[0][0][:len(sf.rows[0])])
+            torch.cuda.synchronize()
     if warm_gather:
         sf.finish()
     torch.cuda.synchronize()
