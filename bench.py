@@ -285,7 +285,7 @@ def pmc_iters_per_call(args, shard_world: int) -> int:
     from pnraytracing_amd.tracer import shard_rows      # (numpy only: loads no library)
     W, H = CONFIG_DIMS[args.config]
     rows = max(len(shard_rows(H, BAND, shard_world, r)) for r in range(shard_world))
-    return iters_per_call(args, rows * W)
+    return iters_per_call(args, rows * W, shards=shard_world)
 
 
 def stored_keyed(path, key, src_hash):
@@ -395,23 +395,40 @@ def cpu_baseline_c1(cpu: dict):
                  "sample": f"C1 256x256 x {f1} frames (1 spp each, depth 4) in {d1:.2f}s"}
 
 
-def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26) -> int:
-    """4-spp iterations per pnrt_render call: as given, else calls of about a whole
-    1080p frame's 16 frames of paths (2^21 paths per frame x 16, rounded down to a
-    power-of-two multiple of 16 frames: 16 frames of a 1080p frame, 32 of a half,
-    64 -- the most a batch holds -- of a quarter or less), and no more frames than
-    one batch's 2^26 path slots take (a whole 4K frame: 8).  Multi-rank runs pass
-    the LARGEST share (ShardedFrame.max_rows), so every rank issues the same calls
-    and therefore the same gathers (batch_slots: a test override).  A call's primary
-    pass, each trace launch's drain and its gather are fixed costs, and a rank of
-    N GPUs renders 1/N of the rows: in the driver's 20-step region
-    (tools/share_bench.py, rank 0's share alone, profiles/r05/s24) 16-frame calls
-    gave a rank 1 542 / 1 667 / 1 792 Msamples/s at N = 8 / 4 / 2 (N = 1: 1 812);
-    64-frame calls 1 688 / 1 773 / 1 811, 32-frame ones at N = 2 1 791-1 813."""
+BATCH_FRAMES_MAX = 128     # pnrt_device.hip WF_MAX_CHUNK_FRAMES: frames per batch at most
+
+
+def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26, shards: int = 1) -> int:
+    """4-spp iterations per pnrt_render call: as given, else
+    * one GPU (shards == 1): calls of about a whole 1080p frame's 16 frames of paths
+      (2^21 paths per frame x 16, rounded down to a power-of-two multiple of 16
+      frames), no more frames than one batch's 2^26 path slots take (a whole 4K
+      frame: 8);
+    * a rank of an N-way split (shards > 1): the timed steps in as few calls as
+      possible, each one batch (at most BATCH_FRAMES_MAX frames and 2^26 path
+      slots), split evenly -- in the driver's 20-step region one 20-iteration call
+      at N = 4 / 8 (80 frames of a quarter / eighth), two of 10 at N = 2.
+    Multi-rank runs pass the LARGEST share (ShardedFrame.max_rows), so every rank
+    issues the same calls and therefore the same gathers (batch_slots: a test
+    override).  A call's primary pass, each trace launch's drain and its gather are
+    fixed costs, and a rank of N GPUs renders 1/N of the rows: rank 0's share through
+    bench.py's gather path (tools/share_bench.py --collective, profiles/r06/h/): at
+    N = 8 16-iteration calls (64-frame batches) 1 710-1 771 Msamples/s per rank, one
+    20-iteration call in one 80-frame batch 1 781-1 815; N = 4 1 811-1 871 -> 1 882-
+    1 891; N = 2 calls of 10 instead of 8 +0.7 to +1.7 %.  On one GPU the call size
+    is neutral within the box spread (4 / 5 / 10 / 20 iterations: 1 870-1 920,
+    profiles/r06/h/share_r06h2.txt), so the headline keeps its 16-frame calls."""
     if args.iters_per_call > 0:
         return args.iters_per_call
-    scale = max(1, min(4, (1 << 21) // max(1, paths_per_frame)))
-    frames = min(16 * scale, batch_slots // max(1, paths_per_frame))
+    ppf = max(1, paths_per_frame)
+    batch_frames = min(BATCH_FRAMES_MAX, batch_slots // ppf)
+    if shards > 1:
+        most = max(1, batch_frames // 4)
+        steps = max(1, getattr(args, "steps", most))
+        ncalls = -(-steps // most)
+        return -(-steps // ncalls)
+    scale = max(1, min(4, (1 << 21) // ppf))
+    frames = min(16 * scale, batch_frames)
     return max(1, min(16, frames // 4))
 
 
@@ -700,7 +717,7 @@ def main(argv=None):
     image = None
 
     # every rank plans its calls from the LARGEST share, so all issue the same gathers
-    ipc = iters_per_call(args, sf.max_rows * W)
+    ipc = iters_per_call(args, sf.max_rows * W, shards=world)
     if world > 1:
         same_on_all_ranks([ipc, len(call_groups(0, args.warmup, ipc)),
                            len(call_groups(args.warmup, args.warmup + args.steps, ipc))],

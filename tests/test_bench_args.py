@@ -17,16 +17,28 @@ def _bench():
 
 def test_iters_per_call_defaults():
     b = _bench()
-    ns = type("A", (), {"iters_per_call": 0})()
+    ns = type("A", (), {"iters_per_call": 0, "steps": 20})()
     assert b.iters_per_call(ns, 1920 * 1080) == 4          # 16 frames of 1080p: one batch
-    assert b.iters_per_call(ns, 1920 * 540) == 8           # N = 2 shares: 32 frames
-    for n in (4, 8):
-        assert b.iters_per_call(ns, 1920 * (1080 // n)) == 16  # N = 4, 8: 64 frames, a batch's most
     assert b.iters_per_call(ns, 3840 * 2160) == 2          # 4K: 8 frames per batch
-    assert b.iters_per_call(ns, 3840 * 270) == 8           # a rank's 4K share at N = 8: 32 frames
     assert b.iters_per_call(ns, 8192 * 4320) == 1          # one frame per batch
+    # a rank's share of an N-way split: the timed steps in as few one-batch calls as fit
+    # (at most BATCH_FRAMES_MAX frames and 2^26 path slots), split evenly
+    assert b.iters_per_call(ns, 1920 * 544, shards=2) == 10      # 64 frames a batch: 2 calls of 10
+    for n in (4, 8):
+        assert b.iters_per_call(ns, 1920 * (1080 // n), shards=n) == 20   # one 80-frame call
+    assert b.iters_per_call(ns, 3840 * 272, shards=8) == 10     # a 4K share: 64 frames a batch
+    ns.steps = 100
+    assert b.iters_per_call(ns, 1920 * 136, shards=8) == 25     # 4 calls of 100 frames
+    assert b.iters_per_call(ns, 1920 * 544, shards=2) == 15     # 7 calls (15 x 6 + 10)
+    for steps in range(1, 90):
+        ns.steps = steps
+        for rows, n in ((544, 2), (272, 4), (136, 8)):
+            ipc = b.iters_per_call(ns, 1920 * rows, shards=n)
+            assert 4 * ipc <= min(b.BATCH_FRAMES_MAX, (1 << 26) // (1920 * rows))   # every call one batch
+            assert -(-steps // ipc) == -(-steps // (min(b.BATCH_FRAMES_MAX, (1 << 26) // (1920 * rows)) // 4))
     ns.iters_per_call = 3
     assert b.iters_per_call(ns, 1920 * 1080) == 3 and b.iters_per_call(ns, 3840 * 2160) == 3
+    assert b.iters_per_call(ns, 1920 * 136, shards=8) == 3
 
 
 def test_call_groups_cover_exactly_the_region():
@@ -133,12 +145,12 @@ def test_step_rooflines():
 
 def test_pmc_child_runs_the_timed_call_size():
     """at N > 1 rank 0's PMC child renders its share in calls of the size
-    the timed run issues (32 frames at N = 2, 64 at N >= 4), passed explicitly, with
+    the timed run issues (driver's 20 steps: 40 frames at N = 2, 80 at N >= 4), passed explicitly, with
     2 calls timed after 1 of warm-up -- so bytes per launch and launches per step
     are those of the timed launches."""
     b = _bench()
-    for n, ipc in ((1, 4), (2, 8), (4, 16), (8, 16)):
-        a = b.parse(["--gpus", str(n)])
+    for n, ipc in ((1, 4), (2, 10), (4, 20), (8, 20)):
+        a = b.parse(["--gpus", str(n), "--steps", "20"])
         cmd = b.pmc_child_cmd(a, n, "rocprofv3", ("FETCH_SIZE",), "/tmp/x")
         i = cmd.index("--child")
         child = cmd[i:]
@@ -148,7 +160,7 @@ def test_pmc_child_runs_the_timed_call_size():
         # the timed run's own call size for rank 0's share (ShardedFrame.max_rows x W)
         from pnraytracing_amd.tracer import shard_rows
         rows = max(len(shard_rows(1080, b.BAND, n, r)) for r in range(n))
-        assert b.iters_per_call(a, rows * 1920) == ipc
+        assert b.iters_per_call(a, rows * 1920, shards=n) == ipc
     assert b.pmc_iters_per_call(b.parse(["--config", "C5"]), 1) == 2
     assert b.pmc_iters_per_call(b.parse(["--config", "D2"]), 1) == 1
     assert b.pmc_iters_per_call(b.parse(["--iters-per-call", "3"]), 4) == 3

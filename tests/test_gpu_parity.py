@@ -206,13 +206,13 @@ def test_large_frame_batches(pt):
 
 
 def test_many_frames_and_calls(pt):
-    """One call of 70 frames (two frame groups: batches of <= 64 frames) and six
+    """One call of 140 frames (two frame groups: batches of <= 128 frames) and six
     calls in a row (the pipelined buffer sets rotate twice) both equal the
-    oracle's 70 / 12-frame progressive means."""
+    oracle's 140 / 12-frame progressive means."""
     c = cfg("C2", width=80, height=48, spp=4)
-    got = gpu_render(pt, c, 0, 70)
-    ref, _ = pyoracle.Oracle(c).render(0, 70)
-    assert_bitwise(got, ref, "render(0, 70)")
+    got = gpu_render(pt, c, 0, 140)
+    ref, _ = pyoracle.Oracle(c).render(0, 140)
+    assert_bitwise(got, ref, "render(0, 140)")
     pt.reset_accum()
     for k in range(6):
         pt.render(2 * k, 2)
