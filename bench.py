@@ -442,9 +442,9 @@ def sizing_calls(warmup: int, steps: int, ipc: int):
     """Iterations of the untimed calls issued before the warm-up: one per distinct call
     size of the warm-up and timed plans, the timed calls' size first.  A call size
     selects how many buffer sets ("pipes") calls of that size rotate over (by paths per
-    batch), and the first call of a size sizes all of them -- so the cut last call of a
-    plan (e.g. 4 iterations after a 16-iteration call at N = 8) allocates nothing inside
-    the timed region."""
+    batch), and the first call of a size sizes all of them -- so neither a shorter
+    warm-up call (5 iterations beside the 20-iteration timed call of an N = 8 share)
+    nor the cut last call of a plan allocates inside the warm-up or the timed region."""
     sizes = {m for _, m in call_groups(0, warmup, ipc) + call_groups(warmup, warmup + steps, ipc)}
     return [ipc] + sorted(sizes - {ipc}, reverse=True)
 
