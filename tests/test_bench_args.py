@@ -179,3 +179,14 @@ def test_issue_stats_and_valu_bound():
     assert b.derive_bound(0.15, 0.8, 0.4, 0.98, 0.5) == "l2-latency"
     assert b.derive_bound(0.6, 0.8, 0.4, 0.98, 0.7) == "hbm"
     assert b.derive_bound(0.27, 0.5, 0.4, 0.87, None) == "hbm-latency"
+
+
+def test_batch_frames_match_the_library():
+    """bench.BATCH_FRAMES_MAX (the share call plan's one-batch limit) is the library's
+    WF_MAX_CHUNK_FRAMES: a plan computed against a larger limit would split a share's
+    call into two batches (profiles/r06/h/summary.txt)."""
+    import re
+    b = _bench()
+    src = open(os.path.join(REPO, "pnraytracing_amd", "csrc", "pnrt_device.hip")).read()
+    m = re.search(r"#define WF_MAX_CHUNK_FRAMES (\d+)", src)
+    assert m and int(m.group(1)) == b.BATCH_FRAMES_MAX
