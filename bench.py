@@ -400,36 +400,34 @@ BATCH_FRAMES_MAX = 128     # pnrt_device.hip WF_MAX_CHUNK_FRAMES: frames per bat
 
 def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26, shards: int = 1) -> int:
     """4-spp iterations per pnrt_render call: as given, else
-    * one GPU (shards == 1): calls of about a whole 1080p frame's 16 frames of paths
-      (2^21 paths per frame x 16, rounded down to a power-of-two multiple of 16
-      frames), no more frames than one batch's 2^26 path slots take (a whole 4K
-      frame: 8);
-    * a rank of an N-way split (shards > 1): the timed steps in as few calls as
-      possible, each one batch (at most BATCH_FRAMES_MAX frames and 2^26 path
-      slots), split evenly -- in the driver's 20-step region one 20-iteration call
-      at N = 4 / 8 (80 frames of a quarter / eighth), two of 10 at N = 2.
+    * one GPU (shards == 1): calls of one whole batch -- as many frames as one
+      batch holds (at most BATCH_FRAMES_MAX frames and 2^26 path slots: 32 frames
+      of a 1080p frame, 8 of a 4K frame), the last call cut at the region's end;
+    * a rank of an N-way split (shards > 1): the timed steps in as few one-batch
+      calls as fit, split evenly -- in the driver's 20-step region one 20-iteration
+      call at N = 4 / 8 (80 frames of a quarter / eighth), two of 10 at N = 2.
     Multi-rank runs pass the LARGEST share (ShardedFrame.max_rows), so every rank
     issues the same calls and therefore the same gathers (batch_slots: a test
-    override).  A call's primary pass, each trace launch's drain and its gather are
-    fixed costs, and a rank of N GPUs renders 1/N of the rows: rank 0's share through
-    bench.py's gather path (tools/share_bench.py --collective, profiles/r06/h/): at
-    N = 8 16-iteration calls (64-frame batches) 1 710-1 771 Msamples/s per rank, one
-    20-iteration call in one 80-frame batch 1 781-1 815; N = 4 1 811-1 871 -> 1 882-
-    1 891; N = 2 calls of 10 instead of 8 +0.7 to +1.7 %.  On one GPU the call size
-    is neutral within the box spread (4 / 5 / 10 / 20 iterations: 1 870-1 920,
-    profiles/r06/h/share_r06h2.txt), so the headline keeps its 16-frame calls."""
+    override).  A batch's trace launches' drains and its gen / blend launches are
+    fixed costs, so the larger the batch the smaller their share.  Measured
+    (profiles/r06/h/, profiles/r06/j/): one GPU, bench.py C2, 3 rounds: 16-frame calls
+    (the rounds-2..6 plan) 1 887-1 893 Msamples/s, 24 / 28 1 898-1 905, 32 (8 + 8 + 4
+    iterations) 1 921-1 928, 40 (32 + 8-frame batches) 1 898-1 904; C3 / C4 with
+    32-frame calls +1.2 to +1.8 / +2.9 %.  Rank 0's share through bench.py's gather path
+    (tools/share_bench.py --collective): N = 8 16-iteration calls (64-frame batches)
+    1 710-1 771 per rank, one 20-iteration call in one 80-frame batch 1 781-1 815;
+    N = 4 1 811-1 871 -> 1 882-1 891; N = 2 calls of 10 1 890-1 897 against 16 + 4
+    1 860-1 868 (the even split wins there, the whole-batch rule on one GPU: 7 + 7 + 6
+    iterations 1 898-1 905 against 8 + 8 + 4)."""
     if args.iters_per_call > 0:
         return args.iters_per_call
     ppf = max(1, paths_per_frame)
-    batch_frames = min(BATCH_FRAMES_MAX, batch_slots // ppf)
+    most = max(1, min(BATCH_FRAMES_MAX, batch_slots // ppf) // 4)
     if shards > 1:
-        most = max(1, batch_frames // 4)
         steps = max(1, getattr(args, "steps", most))
         ncalls = -(-steps // most)
         return -(-steps // ncalls)
-    scale = max(1, min(4, (1 << 21) // ppf))
-    frames = min(16 * scale, batch_frames)
-    return max(1, min(16, frames // 4))
+    return most
 
 
 def call_groups(lo: int, hi: int, ipc: int):

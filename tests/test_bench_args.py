@@ -18,9 +18,10 @@ def _bench():
 def test_iters_per_call_defaults():
     b = _bench()
     ns = type("A", (), {"iters_per_call": 0, "steps": 20})()
-    assert b.iters_per_call(ns, 1920 * 1080) == 4          # 16 frames of 1080p: one batch
+    assert b.iters_per_call(ns, 1920 * 1080) == 8          # one GPU: a whole batch, 32 frames of 1080p
     assert b.iters_per_call(ns, 3840 * 2160) == 2          # 4K: 8 frames per batch
     assert b.iters_per_call(ns, 8192 * 4320) == 1          # one frame per batch
+    assert b.iters_per_call(ns, 512 * 512) == 32           # small frames: BATCH_FRAMES_MAX frames
     # a rank's share of an N-way split: the timed steps in as few one-batch calls as fit
     # (at most BATCH_FRAMES_MAX frames and 2^26 path slots), split evenly
     assert b.iters_per_call(ns, 1920 * 544, shards=2) == 10      # 64 frames a batch: 2 calls of 10
@@ -149,7 +150,7 @@ def test_pmc_child_runs_the_timed_call_size():
     2 calls timed after 1 of warm-up -- so bytes per launch and launches per step
     are those of the timed launches."""
     b = _bench()
-    for n, ipc in ((1, 4), (2, 10), (4, 20), (8, 20)):
+    for n, ipc in ((1, 8), (2, 10), (4, 20), (8, 20)):
         a = b.parse(["--gpus", str(n), "--steps", "20"])
         cmd = b.pmc_child_cmd(a, n, "rocprofv3", ("FETCH_SIZE",), "/tmp/x")
         i = cmd.index("--child")

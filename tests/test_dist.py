@@ -82,11 +82,11 @@ def _plan_worker(rank, world, port, w, h, band, slots, spp, warm, steps, out_pat
     try:
         tr = OracleTracer(S.cornell_c1(w, h))
         sf = ShardedFrame(tr, band=band, device="cpu")
-        ns = type("A", (), {"iters_per_call": 0})()
+        ns = type("A", (), {"iters_per_call": 0, "steps": steps})()
         own = [None] * world                      # what each rank would plan from its OWN share
-        dist.all_gather_object(own, bench.iters_per_call(ns, sf.my_rows * w, batch_slots=slots))
+        dist.all_gather_object(own, bench.iters_per_call(ns, sf.my_rows * w, batch_slots=slots, shards=world))
         assert len(set(own)) > 1, own             # the hazard is present in this frame
-        ipc = bench.iters_per_call(ns, sf.max_rows * w, batch_slots=slots)
+        ipc = bench.iters_per_call(ns, sf.max_rows * w, batch_slots=slots, shards=world)   # as bench.py
         bench.same_on_all_ranks([ipc, len(bench.call_groups(0, warm, ipc)),
                                  len(bench.call_groups(warm, warm + steps, ipc))], "cpu")
         n = bench.issue_calls(sf, spp, 0, warm, ipc, world)
@@ -110,7 +110,7 @@ def test_bench_gather_count_same_on_every_rank(tmp_path):
     import pyoracle
     from pnraytracing_amd import scenes as S
     w, h, band, spp, warm, steps = 40, 44, 8, 2, 1, 3
-    slots = 20 * w * 8            # rank 1's 20 rows fit 8 frames (2 iterations), rank 0's 24 only 6 (1)
+    slots = 20 * w * 8            # rank 1's 20 rows fit 8 frames (calls of 2 iterations), rank 0's 24 only 6 (1)
     out = str(tmp_path / "img.npy")
     mp.start_processes(_plan_worker, args=(2, _free_port(), w, h, band, slots, spp, warm, steps, out), nprocs=2,
                        join=True, start_method="spawn")

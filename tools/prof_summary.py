@@ -5,9 +5,11 @@ kernel_ms must be reproducible from the committed rocprof record).
 
 bench.py issues one untimed sizing call before its warm-up (cold caches and
 first-touch pages make its launches slower); the summary therefore reports
-every launch AND the launches after that first call.  With `--serial --warmup 4
---steps 8` every call is a whole 16-frame call in flight alone, so the trace
-kernel's average over the later launches is the line's exclusive kernel_ms.
+every launch AND the launches after that first call.  With `--serial --warmup 8
+--steps 16` (tools/gpu_session.sh prof) every call is a whole one-batch call of the
+bench's size (8 iterations, 32 frames of 1080p; 16 frames until late round 6) in
+flight alone, so the trace kernel's average over the later launches is the line's
+exclusive kernel_ms.
 
     python tools/prof_summary.py KERNEL_TRACE.csv BENCH_LINE.json [OUT.json] [--serial]
 
