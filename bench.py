@@ -396,38 +396,39 @@ def cpu_baseline_c1(cpu: dict):
 
 
 BATCH_FRAMES_MAX = 128     # pnrt_device.hip WF_MAX_CHUNK_FRAMES: frames per batch at most
+BATCH_SLOTS = 1 << 28      # pt_wf.h WF_SLOT_BITS: path slots per batch at most
 
 
-def iters_per_call(args, paths_per_frame: int, batch_slots: int = 1 << 26, shards: int = 1) -> int:
+def iters_per_call(args, paths_per_frame: int, batch_slots: int = BATCH_SLOTS, shards: int = 1) -> int:
     """4-spp iterations per pnrt_render call: as given, else
     * one GPU (shards == 1): calls of one whole batch -- as many frames as one
-      batch holds (at most BATCH_FRAMES_MAX frames and 2^26 path slots: 32 frames
-      of a 1080p frame, 8 of a 4K frame), the last call cut at the region's end;
+      batch holds (at most BATCH_FRAMES_MAX frames and BATCH_SLOTS path slots: 128
+      frames of a 1080p frame, 32 of a 4K frame) but no more than the steps, the last
+      call cut at the region's end (the driver's 20 steps of C2: one 80-frame call);
     * a rank of an N-way split (shards > 1): the timed steps in as few one-batch
-      calls as fit, split evenly -- in the driver's 20-step region one 20-iteration
-      call at N = 4 / 8 (80 frames of a quarter / eighth), two of 10 at N = 2.
+      calls as fit, split evenly (20 steps: one call at every N).
     Multi-rank runs pass the LARGEST share (ShardedFrame.max_rows), so every rank
     issues the same calls and therefore the same gathers (batch_slots: a test
     override).  A batch's trace launches' drains and its gen / blend launches are
     fixed costs, so the larger the batch the smaller their share.  Measured
-    (profiles/r06/h/, profiles/r06/j/): one GPU, bench.py C2, 3 rounds: 16-frame calls
-    (the rounds-2..6 plan) 1 887-1 893 Msamples/s, 24 / 28 1 898-1 905, 32 (8 + 8 + 4
-    iterations) 1 921-1 928, 40 (32 + 8-frame batches) 1 898-1 904; C3 / C4 with
-    32-frame calls +1.2 to +1.8 / +2.9 %.  Rank 0's share through bench.py's gather path
+    (profiles/r06/h/, profiles/r06/j/, profiles/r06/k/): one GPU, bench.py C2, same box:
+    16-frame calls (the plan since round 2) 1 887-1 893 Msamples/s, 32-frame calls
+    (a whole batch of 2^26 slots) 1 921-1 928; with 2^28-slot batches one 80-frame
+    call 1 915-1 926 against 1 893-1 897 for 32-frame calls (another box), C3 +1.1
+    to +2 %, C5 8 frames -> 32 +2.2 %.  Rank 0's share through bench.py's gather path
     (tools/share_bench.py --collective): N = 8 16-iteration calls (64-frame batches)
     1 710-1 771 per rank, one 20-iteration call in one 80-frame batch 1 781-1 815;
-    N = 4 1 811-1 871 -> 1 882-1 891; N = 2 calls of 10 1 890-1 897 against 16 + 4
-    1 860-1 868 (the even split wins there, the whole-batch rule on one GPU: 7 + 7 + 6
-    iterations 1 898-1 905 against 8 + 8 + 4)."""
+    N = 4 1 811-1 871 -> 1 882-1 891; N = 2 two calls of 10 1 890-1 897 against
+    16 + 4 1 860-1 868 (even split; on one GPU 8 + 8 + 4 beat 7 + 7 + 6)."""
     if args.iters_per_call > 0:
         return args.iters_per_call
     ppf = max(1, paths_per_frame)
     most = max(1, min(BATCH_FRAMES_MAX, batch_slots // ppf) // 4)
+    steps = max(1, getattr(args, "steps", most))
     if shards > 1:
-        steps = max(1, getattr(args, "steps", most))
         ncalls = -(-steps // most)
         return -(-steps // ncalls)
-    return most
+    return min(most, steps)
 
 
 def call_groups(lo: int, hi: int, ipc: int):

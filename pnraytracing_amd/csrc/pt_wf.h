@@ -75,10 +75,16 @@ PN_DEV float4 ps_ld(const float4* p) {
 #define WF_RENV 4u
 #define WF_RCONT 8u
 // ... and the path's meta word, P6.w: slot (pixel, frame) | light ray | env ray | bounce
-#define WF_META_SLOT 0x03ffffffu
-#define WF_META_RL (1u << 26)
-#define WF_META_RE (1u << 27)
-#define WF_META_BSHIFT 28
+// (WF_SLOT_BITS bits of slot bound the paths of one batch; the bounce takes the top
+// bits above the two ray flags: 2 bits hold pnrt_set_frame's depth <= 4)
+#ifndef WF_SLOT_BITS
+#define WF_SLOT_BITS 28      // 2^28 paths per batch: 128 frames of a 1080p frame, 32 of a 4K frame (26 until late round 6)
+#endif
+static_assert(WF_SLOT_BITS >= 20 && WF_SLOT_BITS <= 28, "slot | RL | RE | bounce (>= 2 bits) in 32");
+#define WF_META_SLOT ((1u << WF_SLOT_BITS) - 1u)
+#define WF_META_RL (1u << WF_SLOT_BITS)
+#define WF_META_RE (1u << (WF_SLOT_BITS + 1))
+#define WF_META_BSHIFT (WF_SLOT_BITS + 2)
 
 // Path state between a setup and the next shade: exactly what shade reads,
 // 112 B per live path (the primary hit's base colour is re-read from the
@@ -763,7 +769,7 @@ struct TravState {
 
 template <bool TBL>
 PN_DEV bool wf_has_tri(const TravState& t) { return TBL ? t.lc > 0 : (uint32_t)t.lt >= (REF_LEAF | (1u << 24)); }
-#define WF_RID_P 0x03ffffffu          // TravState::rid: kind << 30 | flags | path entry (< 2^26)
+#define WF_RID_P WF_META_SLOT         // TravState::rid: kind << 30 | flags | path entry (< 2^WF_SLOT_BITS)
 #define WF_RID_NOCOOP (1u << 29)      // the cooperative finish gave this ray back (traced alone to the end)
 // A ray (t.r set) starts: the root box test (:433), tMax, no hit, empty stack.
 template <bool TBL>

@@ -18,25 +18,28 @@ def _bench():
 def test_iters_per_call_defaults():
     b = _bench()
     ns = type("A", (), {"iters_per_call": 0, "steps": 20})()
-    assert b.iters_per_call(ns, 1920 * 1080) == 8          # one GPU: a whole batch, 32 frames of 1080p
-    assert b.iters_per_call(ns, 3840 * 2160) == 2          # 4K: 8 frames per batch
-    assert b.iters_per_call(ns, 8192 * 4320) == 1          # one frame per batch
-    assert b.iters_per_call(ns, 512 * 512) == 32           # small frames: BATCH_FRAMES_MAX frames
-    # a rank's share of an N-way split: the timed steps in as few one-batch calls as fit
-    # (at most BATCH_FRAMES_MAX frames and 2^26 path slots), split evenly
-    assert b.iters_per_call(ns, 1920 * 544, shards=2) == 10      # 64 frames a batch: 2 calls of 10
-    for n in (4, 8):
-        assert b.iters_per_call(ns, 1920 * (1080 // n), shards=n) == 20   # one 80-frame call
-    assert b.iters_per_call(ns, 3840 * 272, shards=8) == 10     # a 4K share: 64 frames a batch
+    # one GPU: a whole batch (BATCH_FRAMES_MAX frames, BATCH_SLOTS paths), no more than the steps
+    assert b.iters_per_call(ns, 1920 * 1080) == 20         # 128 frames of 1080p fit: one 80-frame call
+    assert b.iters_per_call(ns, 3840 * 2160) == 8          # 4K: 32 frames per batch
+    assert b.iters_per_call(ns, 8192 * 4320) == 1          # 7 frames per batch: one iteration
+    assert b.iters_per_call(ns, 512 * 512) == 20
+    assert b.iters_per_call(ns, 1920 * 1080, batch_slots=1 << 26) == 8    # 2^26 slots: 32 frames
+    # a rank's share of an N-way split: the timed steps in as few one-batch calls as fit, split evenly
+    for n in (2, 4, 8):
+        assert b.iters_per_call(ns, 1920 * (1080 // n), shards=n) == 20   # one call
+    assert b.iters_per_call(ns, 1920 * 544, shards=2, batch_slots=1 << 26) == 10   # 64 frames: 2 calls of 10
     ns.steps = 100
+    assert b.iters_per_call(ns, 1920 * 1080) == 32         # 32 + 32 + 32 + 4
     assert b.iters_per_call(ns, 1920 * 136, shards=8) == 25     # 4 calls of 100 frames
-    assert b.iters_per_call(ns, 1920 * 544, shards=2) == 15     # 7 calls (15 x 6 + 10)
-    for steps in range(1, 90):
-        ns.steps = steps
-        for rows, n in ((544, 2), (272, 4), (136, 8)):
-            ipc = b.iters_per_call(ns, 1920 * rows, shards=n)
-            assert 4 * ipc <= min(b.BATCH_FRAMES_MAX, (1 << 26) // (1920 * rows))   # every call one batch
-            assert -(-steps // ipc) == -(-steps // (min(b.BATCH_FRAMES_MAX, (1 << 26) // (1920 * rows)) // 4))
+    assert b.iters_per_call(ns, 3840 * 2160) == 8
+    for slots in (1 << 26, b.BATCH_SLOTS):
+        for steps in range(1, 90):
+            ns.steps = steps
+            for rows, n in ((1080, 1), (544, 2), (272, 4), (136, 8)):
+                ipc = b.iters_per_call(ns, 1920 * rows, shards=n, batch_slots=slots)
+                fit = min(b.BATCH_FRAMES_MAX, slots // (1920 * rows))
+                assert 4 * ipc <= fit                                  # every call one batch
+                assert -(-steps // ipc) == -(-steps // (fit // 4))     # as few calls as fit
     ns.iters_per_call = 3
     assert b.iters_per_call(ns, 1920 * 1080) == 3 and b.iters_per_call(ns, 3840 * 2160) == 3
     assert b.iters_per_call(ns, 1920 * 136, shards=8) == 3
@@ -146,11 +149,11 @@ def test_step_rooflines():
 
 def test_pmc_child_runs_the_timed_call_size():
     """at N > 1 rank 0's PMC child renders its share in calls of the size
-    the timed run issues (driver's 20 steps: 40 frames at N = 2, 80 at N >= 4), passed explicitly, with
+    the timed run issues (driver's 20 steps: one 80-frame call at every N), passed explicitly, with
     2 calls timed after 1 of warm-up -- so bytes per launch and launches per step
     are those of the timed launches."""
     b = _bench()
-    for n, ipc in ((1, 8), (2, 10), (4, 20), (8, 20)):
+    for n, ipc in ((1, 20), (2, 20), (4, 20), (8, 20)):
         a = b.parse(["--gpus", str(n), "--steps", "20"])
         cmd = b.pmc_child_cmd(a, n, "rocprofv3", ("FETCH_SIZE",), "/tmp/x")
         i = cmd.index("--child")
@@ -162,7 +165,7 @@ def test_pmc_child_runs_the_timed_call_size():
         from pnraytracing_amd.tracer import shard_rows
         rows = max(len(shard_rows(1080, b.BAND, n, r)) for r in range(n))
         assert b.iters_per_call(a, rows * 1920, shards=n) == ipc
-    assert b.pmc_iters_per_call(b.parse(["--config", "C5"]), 1) == 2
+    assert b.pmc_iters_per_call(b.parse(["--config", "C5"]), 1) == 8      # 32 4K frames a batch
     assert b.pmc_iters_per_call(b.parse(["--config", "D2"]), 1) == 1
     assert b.pmc_iters_per_call(b.parse(["--iters-per-call", "3"]), 4) == 3
 
@@ -183,11 +186,14 @@ def test_issue_stats_and_valu_bound():
 
 
 def test_batch_frames_match_the_library():
-    """bench.BATCH_FRAMES_MAX (the share call plan's one-batch limit) is the library's
-    WF_MAX_CHUNK_FRAMES: a plan computed against a larger limit would split a share's
-    call into two batches (profiles/r06/h/summary.txt)."""
+    """bench.BATCH_FRAMES_MAX / BATCH_SLOTS (the call plan's one-batch limits) are the
+    library's WF_MAX_CHUNK_FRAMES / 2^WF_SLOT_BITS: a plan computed against a larger
+    limit would split a call into two batches (profiles/r06/h/summary.txt)."""
     import re
     b = _bench()
     src = open(os.path.join(REPO, "pnraytracing_amd", "csrc", "pnrt_device.hip")).read()
     m = re.search(r"#define WF_MAX_CHUNK_FRAMES (\d+)", src)
     assert m and int(m.group(1)) == b.BATCH_FRAMES_MAX
+    wf = open(os.path.join(REPO, "pnraytracing_amd", "csrc", "pt_wf.h")).read()
+    m = re.search(r"#define WF_SLOT_BITS (\d+)", wf)
+    assert m and 1 << int(m.group(1)) == b.BATCH_SLOTS

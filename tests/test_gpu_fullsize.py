@@ -153,3 +153,22 @@ def test_set_stream_between_pipelined_calls(pt):
     pt.set_stream(None)                    # back to the context's own stream
     pt.render(6, 2)
     assert_bitwise(pt.read_accum(), ref, "stream switches mid-sequence")
+
+
+def test_batch_beyond_2_26_paths(pt):
+    """One call of 40 frames of the 1080p C4 frame is ONE batch of 83M paths --
+    path entries above 2^26, the 28-bit slot and ray-id fields (pt_wf.h
+    WF_SLOT_BITS) -- and equals the same 40 frames rendered as five 8-frame calls
+    (batches of 16.6M paths, which the rest of the suite pins to the oracle), bit
+    for bit; two of its rows are checked against the oracle as well."""
+    c = cfg("C4")
+    big = gpu_render(pt, c, 0, 40)
+    pt.reset_accum()
+    for k in range(5):
+        pt.render(8 * k, 8)
+    small = pt.read_accum()
+    assert_bitwise(big, small, "C4 40 frames: one 83M-path batch vs 8-frame calls")
+    o = pyoracle.Oracle(c)
+    for y in (0, 701):
+        ref, _ = o.render(0, 40, rows=(y, y + 1))
+        assert_bitwise(big[y:y + 1], ref[y:y + 1], f"C4 40 frames, row {y}: one batch vs oracle")
