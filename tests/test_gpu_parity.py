@@ -190,19 +190,20 @@ def test_progressive_split_calls(pt):
 
 
 def test_large_frame_batches(pt):
-    """An 8192x4320 frame holds more path slots than fit two frames in one batch
-    (2^26), so a full-frame call renders one frame per batch; a 1/16 row shard
-    of the same call fits all three frames in one batch.  Its rows must match."""
+    """An 8192x4320 frame (35.4M path slots) fits 7 frames in one batch (2^28
+    slots), so a full-frame call of 9 frames renders batches of 7 + 2 frames; a
+    1/16 row shard of the same call fits all nine in one batch.  Its rows must
+    match."""
     c = S.bunny_c2(8192, 4320)
     pt.load(c)
     pt.reset_accum()
-    pt.render(0, 3)
+    pt.render(0, 9)
     full = pt.read_accum()
     pt.reset_accum()
-    pt.render(0, 3, 8, 16, 0)
+    pt.render(0, 9, 8, 16, 0)
     part = pt.read_accum()
     rows = (np.arange(c.height) // 8) % 16 == 0
-    assert_bitwise(part[rows], full[rows], "8192x4320: shard (one batch) vs full frame (one frame per batch)")
+    assert_bitwise(part[rows], full[rows], "8192x4320: shard (one batch) vs full frame (batches of 7 + 2 frames)")
 
 
 def test_many_frames_and_calls(pt):
