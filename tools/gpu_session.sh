@@ -119,9 +119,9 @@ for s in ${STEPS:-smoke tests bench}; do
       done ;;
     prof)
       step prof-serial timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_serial -o run --output-format csv -- \
-        python bench.py --steps 16 --warmup 8 --no-cpu-baseline --no-pmc --serial > $O/prof_serial.json 2> $O/prof_serial.err
+        python bench.py --steps 20 --warmup 20 --no-cpu-baseline --no-pmc --serial > $O/prof_serial.json 2> $O/prof_serial.err
       step prof-pipe timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_pipe -o run --output-format csv -- \
-        python bench.py --steps 16 --warmup 8 --no-cpu-baseline --no-pmc > $O/prof_pipe.json 2> $O/prof_pipe.err
+        python bench.py --steps 20 --warmup 20 --no-cpu-baseline --no-pmc > $O/prof_pipe.json 2> $O/prof_pipe.err
       for m in serial pipe; do     # rocprof's trace-kernel average vs the line's kernel_ms (CPU only)
         python3 tools/prof_summary.py $O/prof_$m/run_kernel_trace.csv $O/prof_$m.json $O/prof_${m}_check.json > /dev/null \
           && python3 -c "import json; print('  prof-$m', json.load(open('$O/prof_${m}_check.json'))['check'])"

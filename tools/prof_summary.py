@@ -5,9 +5,9 @@ kernel_ms must be reproducible from the committed rocprof record).
 
 bench.py issues one untimed sizing call before its warm-up (cold caches and
 first-touch pages make its launches slower); the summary therefore reports
-every launch AND the launches after that first call.  With `--serial --warmup 8
---steps 16` (tools/gpu_session.sh prof) every call is a whole one-batch call of the
-bench's size (8 iterations, 32 frames of 1080p; 16 frames until late round 6) in
+every launch AND the launches after that first call.  With `--serial --warmup 20
+--steps 20` (tools/gpu_session.sh prof) every call is a whole one-batch call of the
+bench's size (20 iterations, 80 frames of 1080p; 16 frames until late round 6) in
 flight alone, so the trace kernel's average over the later launches is the line's
 exclusive kernel_ms.
 
