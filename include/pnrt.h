@@ -134,7 +134,11 @@ int pnrt_set_options(pnrt_ctx* ctx, int options);
  * order into the accumulation image with the progressive mean of
  * ray_tracing.comp:988-991.  Shard selector (multi-GPU row bands): only rows
  * y with (y / band_rows) % n_shards == shard are rendered; full image =
- * (band_rows >= 1, n_shards = 1, shard = 0).  Asynchronous on the stream. */
+ * (band_rows >= 1, n_shards = 1, shard = 0).  Asynchronous on the stream.
+ * The frames run in batches of up to 128 frames and 2^28 paths (~310 B of
+ * device memory per path; the environment variable PNRT_BATCH_BYTES, read at a
+ * context's first render, caps one batch's bytes -- the batching changes no
+ * pixel). */
 int pnrt_render(pnrt_ctx* ctx, uint32_t first_frame, uint32_t n_frames, int band_rows,
                 int n_shards, int shard);
 

@@ -141,6 +141,7 @@ struct pnrt_ctx {
     };
     Pipe pipe[WF_PIPES];
     unsigned n_pipes_small = WF_PIPES;     // pipes small calls rotate over (pipes_init)
+    size_t batch_bytes_cap = 0;            // PNRT_BATCH_BYTES: device bytes of one batch's buffers at most (0: none)
     unsigned last_pipe = 0;                // the pipe of the last call
     // bumped by every change of what the primary records depend on besides the
     // frame (camera, size, shard, traversal mode: compared per call): the scene
@@ -514,6 +515,10 @@ static int pipes_init(pnrt_ctx* c) {
     const char* q = getenv("GPU_MAX_HW_QUEUES");
     const int hw_queues = (q && atoi(q) > 0) ? atoi(q) : 4;
     c->n_pipes_small = hw_queues > 4 ? WF_PIPES : WF_PIPES_LARGE;
+    // a caller short of device memory (another tenant, a smaller part) caps one batch's
+    // buffers; frames per batch shrink to fit, which changes no pixel
+    const char* bb = getenv("PNRT_BATCH_BYTES");
+    c->batch_bytes_cap = bb ? (size_t)strtoull(bb, nullptr, 10) : 0;
     for (unsigned i = 0; i < c->n_pipes_small; ++i) {
         auto& P = c->pipe[i];
         HIPCHK(c, hipStreamCreateWithFlags(&P.w, hipStreamNonBlocking));
@@ -540,7 +545,11 @@ static int render_wavefront(pnrt_ctx* c, const DevScene& s, const FrameParams& f
     // slot fits the path state's slot field (large frames take fewer per batch)
     if (per_frame > (size_t)WF_META_SLOT) return set_err(c, PNRT_E_ARG, "render: frame too large for one batch");
     const uint32_t fit = (uint32_t)std::min<size_t>(WF_MAX_CHUNK_FRAMES, (size_t)WF_META_SLOT / per_frame);
-    const uint32_t chunk = nf < fit ? nf : fit;
+    uint32_t chunk = nf < fit ? nf : fit;
+    // (PNRT_BATCH_BYTES: one batch's path state and colours within the cap, down to one frame)
+    while (c->batch_bytes_cap && chunk > 1 &&
+           wf_bytes(per_frame * chunk) + pix * 16 * chunk > c->batch_bytes_cap)
+        chunk = (chunk + 1) / 2;
     // calls in flight by call size (paths per batch): small (< 5M: multi-GPU shares)
     // 4 with > 4 hardware queues; 5M-12M 2 -- their launches are long enough to fill
     // each other's drains (measured on 8-frame 1080p calls before the staggering: C2

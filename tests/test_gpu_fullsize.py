@@ -172,3 +172,20 @@ def test_batch_beyond_2_26_paths(pt):
     for y in (0, 701):
         ref, _ = o.render(0, 40, rows=(y, y + 1))
         assert_bitwise(big[y:y + 1], ref[y:y + 1], f"C4 40 frames, row {y}: one batch vs oracle")
+
+
+def test_batch_bytes_cap(pt):
+    """PNRT_BATCH_BYTES (read when a context first renders) caps one batch's device
+    buffers: a 40-frame C4 call then runs in 14 batches of at most 3 frames
+    (≈ 0.64 GB per 1080p frame) and equals the one-batch call bit for bit."""
+    import os
+    c = cfg("C4")
+    one = gpu_render(pt, c, 0, 40)
+    os.environ["PNRT_BATCH_BYTES"] = str(3 * 10**9)
+    capped = PathTracer(0)
+    try:
+        got = gpu_render(capped, c, 0, 40)
+    finally:
+        capped.close()
+        del os.environ["PNRT_BATCH_BYTES"]
+    assert_bitwise(got, one, "C4 40 frames: 3-frame batches (PNRT_BATCH_BYTES) vs one batch")
