@@ -325,9 +325,11 @@ static inline int fint(float f) { return (int)f; }   // GLSL int(float)
 // Wavefront buffers of one batch of n path slots, carved from `base` (wf_layout):
 // two path-state sets (P0-P7 + block counts), hit / occ, the env ray records,
 // segment counts, dequeue counters + census words (+ the timing builds' stamps).
+#define WF_SOBOL_BYTES (4 * WF_MAX_CHUNK_FRAMES * 8)   // the batch's Sobol table: bounces 1..3 x frames, float2
 static size_t wf_bytes(size_t n) {
     const size_t npad = (n + 255) / 256 * 256, nseg = npad / 256;
-    return 2 * (npad * 16 * 8 + nseg * 4 + 256) + n * (4 + 2) + 256 + npad * 32 + nseg * 12 + 256 + WF_COUNTER_BYTES + 512 +
+    return 2 * (npad * 16 * 8 + nseg * 4 + 256) + n * (4 + 2) + 256 + npad * 32 + nseg * 12 + 256 + WF_SOBOL_BYTES +
+           WF_COUNTER_BYTES + 512 +
            (WF_TIMING ? (size_t)64 * 1024 * 1024 : 0);
 }
 // The two path-state sets of a batch (entries are indexed up to npad: a block's
@@ -362,6 +364,7 @@ static WfLayout wf_layout(char* base, size_t n) {
     b.rayD = reinterpret_cast<float4*>(base + off); off += rec;
     b.segcount = reinterpret_cast<unsigned int*>(base + off); off += (size_t)b.nseg_k * 12;
     off = (off + 255) & ~(size_t)255;
+    b.sobol = reinterpret_cast<float2*>(base + off); off += WF_SOBOL_BYTES;
     b.counter = reinterpret_cast<unsigned int*>(base + off);               // WF_QSHARDS counters, WF_QSTRIDE dwords apart
     b.stats = reinterpret_cast<unsigned long long*>(base + off + WF_COUNTER_BYTES);
     b.n = (uint32_t)n;

@@ -129,6 +129,7 @@ struct WfBufs {
     int chunk_frames;
     int tiles_x;
     uint32_t first_frame;
+    float2* sobol;     // [(bounce - 1) * chunk_frames + k]: the Sobol pair of bounces >= 1, frame k (gen writes it)
 };
 
 // Faults: a trace launch that could leave a queued ray untraced reports it
@@ -388,8 +389,9 @@ PN_DEV uint32_t wf_setup_core(const DevScene& s, const FrameParams& fp, const Wf
     float cpu = rand01(pseed), cpv = rand01(pseed);
     const uint32_t g = (frame + 1u) ^ ((frame + 1u) >> 1);
     float su, sv;
-    if constexpr (SOBOL_PAIR) {
-        sobol_pair(2u * (uint32_t)bounce, g, su, sv);
+    if constexpr (SOBOL_PAIR) {     // (the shade's setups, bounce >= 1: the batch's table, computed once by gen)
+        const float2 v = b.sobol[(uint32_t)(bounce - 1) * (uint32_t)b.chunk_frames + (frame - b.first_frame)];
+        su = v.x; sv = v.y;
     } else {
         su = sobol_dev(2u * (uint32_t)bounce, g);
         sv = sobol_dev(2u * (uint32_t)bounce + 1u, g);
@@ -588,6 +590,16 @@ __global__ void __launch_bounds__(256, WF_GEN_WAVES) pt_wf_gen_setup(DevScene s,
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     // path slot
     wf_reset_counters(b);
     wf_live_init();
+    // the Sobol pairs of bounces 1 .. depth-1 (:539-557) depend only on (bounce, frame):
+    // computed here once per batch, read by the shade kernels' setups (the same
+    // sobol_pair bits each lane would compute)
+    if (i < (uint32_t)max(fp.max_depth - 1, 0) * (uint32_t)b.chunk_frames) {
+        const uint32_t bn = 1u + i / (uint32_t)b.chunk_frames, k = i % (uint32_t)b.chunk_frames;
+        const uint32_t f = b.first_frame + k, gk = (f + 1u) ^ ((f + 1u) >> 1);
+        float su, sv;
+        sobol_pair(2u * bn, gk, su, sv);
+        b.sobol[(bn - 1u) * (uint32_t)b.chunk_frames + k] = make_float2(su, sv);
+    }
     bool cont = false;
     PathIn q;
     int x = 0, py = 0;
